@@ -1,0 +1,220 @@
+"""Headline benchmark: SimCLR pre-training images/sec (whole node), ResNet-50, CIFAR-10 shape.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
+``torch.distributed.run`` (one rank per GPU, RCCL).  W untimed steps, then exactly K timed steps
+bracketed by barrier + device synchronise, max over ranks, rank 0 prints ONE JSON line.
+
+Config (BASELINE.json "ResNet-50 SimCLR CIFAR-10 bf16, batch=512 on 1 MI355X"): ResNet-50 with
+the CIFAR stem (3x3/s1, no maxpool — the north star's CIFAR-ResNet-50), 512 images per GPU (two
+augmented views each → 1024 forward rows), 32x32 synthetic uint8 data augmented on device,
+projection head 2048-2048-128, NT-Xent τ=0.5, LARS + warmup/cosine, full optimizer step inside
+the timed region.  Weak scaling (512 images per GPU at every N).
+
+``--impl reference`` times the reference-semantics step built from stock torch ops (fp32 NCHW,
+two forwards, torch BN/SyncBN, DDP, LARC loop — bench/torch_reference.py) on the same hardware;
+BASELINE publishes no throughput, so that measurement is the ``vs_baseline`` denominator
+(``profiles/reference_baseline.json``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "pretrain images/sec (whole node) + CIFAR-10 linear-probe top-1, ResNet-50"
+
+
+def _init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        be = "nccl" if dev.type == "cuda" else "gloo"
+        kw = {"device_id": dev} if be == "nccl" else {}
+        dist.init_process_group(be, rank=rank, world_size=world, **kw)
+    return rank, world, local, dev
+
+
+def _sync(dev, world):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def run_ours(args, rank, world, dev):
+    from simclr_amd.config import compose, task_config, CONF_DIR
+    from simclr_amd.data.datasets import synthetic_dataset
+    from simclr_amd.data.loader import ContrastiveLoader
+    from simclr_amd.parallel import state as pstate
+    from simclr_amd.train.pretrain import Trainer
+    from simclr_amd.utils.misc import seed_everything
+
+    st = pstate.set_state(rank=rank, world_size=world, local_rank=int(os.environ.get(
+        "LOCAL_RANK", "0")), group=dist.group.WORLD if world > 1 else None,
+        backend=dist.get_backend() if world > 1 else "none")
+    st.device = dev
+    ov = [f"experiment.base_cnn={args.model}", f"experiment.batches={args.batch}",
+          f"model.cifar_stem={'true' if args.cifar_stem else 'null'}",
+          "data.synthetic=true", f"runtime.precision={args.precision}",
+          f"loss.gather={'true' if args.gather else 'false'}", "parameter.epochs=100",
+          f"runtime.bucket_mb={args.bucket_mb}"]
+    cfg = task_config(compose(str(CONF_DIR), "config", ov, job_name="bench"))
+    seed_everything(cfg["parameter"]["seed"])
+    n_img = max(8192, args.batch * world * 2)
+    ds = synthetic_dataset(n_img, 10, size=args.size, seed=rank)
+    loader = ContrastiveLoader(ds, args.batch, dev, rank=rank, world=world,
+                               strength=cfg["experiment"]["strength"], seed=7, views=2)
+    tr = Trainer(cfg, st, 50000)
+    it = iter(loader)
+
+    def next_batch():
+        nonlocal it
+        try:
+            return next(it)[0]
+        except StopIteration:
+            loader.set_epoch(loader.epoch + 1)
+            it = iter(loader)
+            return next(it)[0]
+
+    if args.graph and tr.hip:
+        tr.capture(next_batch())
+    loss = None
+    for _ in range(args.warmup):
+        loss = tr.step(next_batch())
+    _sync(dev, world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.step(next_batch())
+    _sync(dev, world)
+    t1 = time.perf_counter()
+    return t1 - t0, float(loss.item()) if loss is not None else float("nan")
+
+
+def run_reference(args, rank, world, dev):
+    from bench.torch_reference import (PlainContrastive, exclude_from_wt_decay, larc_step,
+                                       nt_xent_reference)
+    torch.manual_seed(7)
+    model = PlainContrastive(args.model, stem="cifar" if args.cifar_stem else "imagenet").to(dev)
+    if world > 1:
+        model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+    opt = torch.optim.SGD(exclude_from_wt_decay(model.named_parameters(), 1e-4),
+                          lr=args.batch / 256, momentum=0.9, weight_decay=0.0)
+    v0 = torch.rand(args.batch, 3, args.size, args.size, device=dev)
+    v1 = torch.rand(args.batch, 3, args.size, args.size, device=dev)
+
+    def step():
+        opt.zero_grad()
+        z0 = model(v0)
+        z1 = model(v1)
+        loss = nt_xent_reference(z0, z1, 0.5)
+        loss.backward()
+        larc_step(opt)
+        return loss
+
+    loss = None
+    for _ in range(args.warmup):
+        loss = step()
+    _sync(dev, world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    _sync(dev, world)
+    return time.perf_counter() - t0, float(loss.item())
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--cifar-stem", dest="cifar_stem", action="store_true", default=True)
+    ap.add_argument("--imagenet-stem", dest="cifar_stem", action="store_false")
+    ap.add_argument("--batch", type=int, default=512, help="images per GPU")
+    ap.add_argument("--size", type=int, default=32)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--gather", action="store_true", help="global negatives (all-gather of z)")
+    ap.add_argument("--graph", action="store_true", default=True)
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--bucket-mb", dest="bucket_mb", type=float, default=32.0)
+    ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
+    args = ap.parse_args(argv)
+    rank, world, local, dev = _init()
+    if args.impl == "ours":
+        dt, loss = run_ours(args, rank, world, dev)
+    else:
+        dt, loss = run_reference(args, rank, world, dev)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ms = dt / args.steps * 1000.0
+    value = args.steps * args.batch * world / dt
+    base = None
+    bpath = ROOT / "profiles" / "reference_baseline.json"
+    if bpath.exists():
+        try:
+            b = json.loads(bpath.read_text())
+            key = f"{args.model}-{'cifar' if args.cifar_stem else 'imagenet'}-b{args.batch}"
+            per_gpu = b.get("images_per_sec_per_gpu", {}).get(key)
+            if per_gpu:
+                base = per_gpu * world
+        except Exception:
+            base = None
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(value / base, 3) if (base and args.impl == "ours") else None),
+        "dtype": args.precision if args.impl == "ours" else "fp32",
+        "data": "synthetic 32x32 uint8 CIFAR-shape images, random-init weights, on-device "
+                "SimCLR augmentation",
+        "config": {
+            "model": f"{args.model}-{'cifar-stem' if args.cifar_stem else 'imagenet-stem'}"
+                     "+projection-head(2048-2048-128)",
+            "global_batch": args.batch * world,
+            "per_gpu_batch": args.batch,
+            "views": 2,
+            "seq_len": None,
+            "image_size": args.size,
+            "parallelism": f"dp{world}",
+            "loss": "nt-xent tau=0.5" + (" global-negatives" if args.gather else " local"),
+            "optimizer": "LARS(trust=1e-3)+SGD(m=0.9), warmup+cosine",
+            "impl": args.impl,
+            "hip_graph": bool(args.graph and args.impl == "ours"),
+            "final_loss": loss,
+        },
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

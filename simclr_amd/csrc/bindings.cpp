@@ -1,0 +1,393 @@
+// torch.ops.simclr_amd.* registrations for the gfx950 kernels.  Every op launches on the current
+// HIP stream (so they compose with hipGraph capture and side-stream overlap) and validates the
+// shapes / dtypes / devices the kernels assume before any launch (a bad shape must never reach a
+// hand-written kernel: an out-of-bounds access can take the whole node down).
+#include <ATen/core/Tensor.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/util/Exception.h>
+#include <torch/library.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+using at::Tensor;
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check_dev(const Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, ": expected a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, ": expected dtype ", dt, " got ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous(), name, ": expected a contiguous tensor");
+}
+
+const uint16_t* bf(const Tensor& t, const char* n) {
+  check_dev(t, at::kBFloat16, n);
+  return reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+uint16_t* bfw(const Tensor& t, const char* n) {
+  check_dev(t, at::kBFloat16, n);
+  return reinterpret_cast<uint16_t*>(t.data_ptr());
+}
+const float* f32(const Tensor& t, const char* n) {
+  check_dev(t, at::kFloat, n);
+  return t.data_ptr<float>();
+}
+float* f32w(const Tensor& t, const char* n) {
+  check_dev(t, at::kFloat, n);
+  return t.data_ptr<float>();
+}
+const float* optf32(const c10::optional<Tensor>& t, const char* n) {
+  return (t.has_value() && t->defined()) ? f32(*t, n) : nullptr;
+}
+float* optf32w(const c10::optional<Tensor>& t, const char* n) {
+  return (t.has_value() && t->defined()) ? f32w(*t, n) : nullptr;
+}
+const uint16_t* optbf(const c10::optional<Tensor>& t, const char* n) {
+  return (t.has_value() && t->defined()) ? bf(*t, n) : nullptr;
+}
+uint16_t* optbfw(const c10::optional<Tensor>& t, const char* n) {
+  return (t.has_value() && t->defined()) ? bfw(*t, n) : nullptr;
+}
+const int* i32(const Tensor& t, const char* n) {
+  check_dev(t, at::kInt, n);
+  return t.data_ptr<int>();
+}
+
+ConvGeom geom_from(const std::vector<int64_t>& v) {
+  TORCH_CHECK(v.size() == 22, "conv geometry must have 22 entries");
+  ConvGeom g;
+  int* p = &g.Nb;
+  for (int i = 0; i < 22; ++i) p[i] = (int)v[i];
+  TORCH_CHECK(g.C % 8 == 0, "conv: gathered channels must be a multiple of 8, got ", g.C);
+  TORCH_CHECK(g.N > 0 && g.Nb > 0 && g.OH > 0 && g.OW > 0, "conv: empty problem");
+  return g;
+}
+
+// ------------------------------------------------------------------------------- conv
+void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optional<Tensor>& bias,
+           const c10::optional<Tensor>& stats, std::vector<int64_t> gv) {
+  const ConvGeom g = geom_from(gv);
+  TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
+  TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
+  const int64_t K = (int64_t)g.KH * g.KW * g.C;
+  TORCH_CHECK(B.numel() == (int64_t)g.N * K, "igemm: B numel mismatch");
+  TORCH_CHECK(g.ldo % 8 == 0 && g.N % 8 == 0, "igemm: N/ldo must be multiples of 8");
+  TORCH_CHECK(out.numel() >= (int64_t)g.Nb * g.OHp * g.OWp * g.ldo, "igemm: out too small");
+  TORCH_CHECK(out.numel() * 2 < ((int64_t)1 << 31) * 2, "igemm: out too large");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
+  if (stats.has_value() && stats->defined()) {
+    const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
+    const int bm = igemm_block_m(g.N);
+    TORCH_CHECK(stats->numel() >= ((M + bm - 1) / bm) * 2 * g.N, "igemm: stats buffer too small");
+  }
+  conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
+                optf32w(stats, "stats"), cur_stream());
+}
+
+int64_t igemm_bm(int64_t N) { return igemm_block_m((int)N); }
+
+int64_t wgrad_nsplit(std::vector<int64_t> gv) { return wgrad_splits(geom_from(gv)); }
+
+void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tensor& out,
+           std::vector<int64_t> gv, int64_t splits, int64_t creal, double beta) {
+  const ConvGeom g = geom_from(gv);
+  const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
+  const int64_t K = (int64_t)g.KH * g.KW * g.C;
+  TORCH_CHECK(dY.numel() == M * g.N, "wgrad: dY numel mismatch");
+  TORCH_CHECK(X.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "wgrad: X numel mismatch");
+  TORCH_CHECK(partial.numel() >= splits * g.N * K, "wgrad: partial too small");
+  TORCH_CHECK(out.numel() == (int64_t)g.N * g.KH * g.KW * creal, "wgrad: out numel mismatch");
+  TORCH_CHECK(creal <= g.C && creal > 0, "wgrad: bad creal");
+  conv_wgrad(g, bf(dY, "dY"), bf(X, "X"), (size_t)X.numel(), f32w(partial, "partial"), (int)splits,
+             f32w(out, "out"), (int)creal, (float)beta, cur_stream());
+}
+
+void weight_transform(const Tensor& W, const Tensor& Wt, std::vector<int64_t> p) {
+  TORCH_CHECK(p.size() == 10, "weight_transform params");
+  const int Co = p[0], KH = p[1], KW = p[2], Ci = p[3], KHs = p[4], KWs = p[5];
+  TORCH_CHECK(W.numel() == (int64_t)Co * KH * KW * Ci, "weight_transform: W numel");
+  TORCH_CHECK(Wt.numel() == (int64_t)Ci * KHs * KWs * Co, "weight_transform: Wt numel");
+  for (int a = 0; a < KHs; ++a) {
+    const int kh = (int)p[6] + a * (int)p[7];
+    TORCH_CHECK(kh >= 0 && kh < KH, "weight_transform: kh out of range");
+  }
+  for (int a = 0; a < KWs; ++a) {
+    const int kw = (int)p[8] + a * (int)p[9];
+    TORCH_CHECK(kw >= 0 && kw < KW, "weight_transform: kw out of range");
+  }
+  conv_weight_transform(bf(W, "W"), bfw(Wt, "Wt"), Co, KH, KW, Ci, KHs, KWs, p[6], p[7], p[8], p[9],
+                        cur_stream());
+}
+
+// ------------------------------------------------------------------------------- batch norm
+void check_rc(const Tensor& x, int64_t S, const char* n) {
+  TORCH_CHECK(x.dim() >= 2, n, ": rank");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0, n, ": channels must be a multiple of 8");
+  const int64_t CH = C / 8;
+  TORCH_CHECK(CH <= 256 || CH % 256 == 0, n, ": unsupported channel count");
+  TORCH_CHECK((x.numel() / C) % S == 0, n, ": rows not divisible by segments");
+}
+
+int64_t bn_blocks(int64_t R, int64_t C, int64_t S) {
+  return bn_stats_blocks_per_seg((int)R, (int)C, (int)S);
+}
+
+void bn_stats(const Tensor& x, int64_t S, const Tensor& partial) {
+  check_rc(x, S, "bn_stats");
+  const int C = x.size(-1), R = x.numel() / C;
+  const int nblk = bn_stats_blocks_per_seg(R, C, S);
+  TORCH_CHECK(partial.numel() >= (int64_t)S * nblk * 2 * C, "bn_stats: partial too small");
+  bn_stats_partial(bf(x, "x"), R, C, S, f32w(partial, "partial"), nullptr, cur_stream());
+}
+
+void bn_reduce(const Tensor& partial, int64_t nblk, int64_t S, int64_t C, const Tensor& stats) {
+  TORCH_CHECK(partial.numel() >= S * nblk * 2 * C && stats.numel() >= 2 * S * C, "bn_reduce sizes");
+  bn_reduce_partials(f32(partial, "partial"), nblk, S, C, f32w(stats, "stats"), cur_stream());
+}
+
+void bn_final(const Tensor& stats, int64_t S, int64_t C, double count, double eps, double momentum,
+              const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv, const Tensor& mi,
+              const c10::optional<Tensor>& nbt) {
+  TORCH_CHECK(stats.numel() >= 2 * S * C && mi.numel() >= 2 * S * C, "bn_finalize sizes");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    check_dev(*nbt, at::kLong, "num_batches_tracked");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  bn_finalize(f32(stats, "stats"), S, C, (float)count, (float)eps, (float)momentum,
+              optf32w(rm, "running_mean"), optf32w(rv, "running_var"), f32w(mi, "mean_invstd"), nb,
+              cur_stream());
+}
+
+void bn_apply_op(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& y,
+                 const Tensor& mi, const c10::optional<Tensor>& gamma,
+                 const c10::optional<Tensor>& beta, int64_t S, bool relu) {
+  check_rc(x, S, "bn_apply");
+  const int C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(y.numel() == x.numel(), "bn_apply: y size");
+  if (res.has_value() && res->defined()) TORCH_CHECK(res->numel() == x.numel(), "bn_apply: res size");
+  TORCH_CHECK(mi.numel() >= 2 * S * C, "bn_apply: mean_invstd size");
+  bn_apply(bf(x, "x"), optbf(res, "res"), bfw(y, "y"), f32(mi, "mi"), optf32(gamma, "gamma"),
+           optf32(beta, "beta"), R, C, S, relu ? 1 : 0, cur_stream());
+}
+
+void bn_apply_eval_op(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& y,
+                      const Tensor& rm, const Tensor& rv, const c10::optional<Tensor>& gamma,
+                      const c10::optional<Tensor>& beta, double eps, bool relu) {
+  check_rc(x, 1, "bn_apply_eval");
+  const int C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(y.numel() == x.numel(), "bn_apply_eval: y size");
+  bn_apply_eval(bf(x, "x"), optbf(res, "res"), bfw(y, "y"), f32(rm, "rm"), f32(rv, "rv"),
+                optf32(gamma, "gamma"), optf32(beta, "beta"), (float)eps, R, C, relu ? 1 : 0,
+                cur_stream());
+}
+
+void bn_bwd_reduce_op(const Tensor& dy, const c10::optional<Tensor>& y, const Tensor& x,
+                      const Tensor& mi, int64_t S, bool relu, const Tensor& partial) {
+  check_rc(x, S, "bn_bwd_reduce");
+  const int C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(dy.numel() == x.numel(), "bn_bwd_reduce: dy size");
+  TORCH_CHECK(!relu || (y.has_value() && y->numel() == x.numel()), "bn_bwd_reduce: y needed");
+  const int nblk = bn_stats_blocks_per_seg(R, C, S);
+  TORCH_CHECK(partial.numel() >= (int64_t)S * nblk * 2 * C, "bn_bwd_reduce: partial too small");
+  bn_bwd_reduce(bf(dy, "dy"), optbf(y, "y"), bf(x, "x"), f32(mi, "mi"), R, C, S, relu ? 1 : 0,
+                f32w(partial, "partial"), cur_stream());
+}
+
+void bn_bwd_final(const Tensor& sums, const Tensor& mi, const c10::optional<Tensor>& gamma,
+                  int64_t S, int64_t C, double count, const c10::optional<Tensor>& dgamma,
+                  const c10::optional<Tensor>& dbeta, const Tensor& coef) {
+  TORCH_CHECK(sums.numel() >= 2 * S * C && coef.numel() >= 3 * S * C, "bn_bwd_finalize sizes");
+  bn_bwd_finalize(f32(sums, "sums"), f32(mi, "mi"), optf32(gamma, "gamma"), S, C, (float)count,
+                  optf32w(dgamma, "dgamma"), optf32w(dbeta, "dbeta"), f32w(coef, "coef"),
+                  cur_stream());
+}
+
+void bn_bwd_apply_op(const Tensor& dy, const c10::optional<Tensor>& y, const Tensor& x,
+                     const Tensor& coef, int64_t S, bool relu, const Tensor& dx,
+                     const c10::optional<Tensor>& dres) {
+  check_rc(x, S, "bn_bwd_apply");
+  const int C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn_bwd_apply sizes");
+  TORCH_CHECK(!relu || (y.has_value() && y->numel() == x.numel()), "bn_bwd_apply: y needed");
+  bn_bwd_apply(bf(dy, "dy"), optbf(y, "y"), bf(x, "x"), f32(coef, "coef"), R, C, S, relu ? 1 : 0,
+               bfw(dx, "dx"), optbfw(dres, "dres"), cur_stream());
+}
+
+// ------------------------------------------------------------------------------- misc
+void avgpool_fwd_op(const Tensor& x, const Tensor& y, int64_t Nb, int64_t HW, int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && x.numel() == Nb * HW * C && y.numel() == Nb * C, "avgpool_fwd sizes");
+  avgpool_fwd(bf(x, "x"), bfw(y, "y"), Nb, HW, C, cur_stream());
+}
+void avgpool_bwd_op(const Tensor& dy, const Tensor& dx, int64_t Nb, int64_t HW, int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && dx.numel() == Nb * HW * C && dy.numel() == Nb * C, "avgpool_bwd sizes");
+  avgpool_bwd(bf(dy, "dy"), bfw(dx, "dx"), Nb, HW, C, cur_stream());
+}
+void colsum_op(const Tensor& x, const Tensor& out, double beta) {
+  const int C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(out.numel() == C, "colsum sizes");
+  colsum_bf16(bf(x, "x"), R, C, f32w(out, "out"), (float)beta, cur_stream());
+}
+void cast_to_bf16(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.numel() == y.numel(), "cast sizes");
+  cast_f32_bf16(f32(x, "x"), bfw(y, "y"), x.numel(), cur_stream());
+}
+void cast_to_f32(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.numel() == y.numel(), "cast sizes");
+  cast_bf16_f32(bf(x, "x"), f32w(y, "y"), x.numel(), cur_stream());
+}
+
+// ------------------------------------------------------------------------------- nt-xent
+void nt_normalize(const Tensor& z, const Tensor& zn, const Tensor& inv_norm) {
+  TORCH_CHECK(z.dim() == 2, "nt_normalize: z must be 2-D");
+  const int R = z.size(0), D = z.size(1);
+  TORCH_CHECK(zn.numel() == (int64_t)R * D && inv_norm.numel() == R, "nt_normalize sizes");
+  ntxent_normalize_f32(bf(z, "z"), R, D, f32w(zn, "zn"), f32w(inv_norm, "inv_norm"), cur_stream());
+}
+void nt_transpose(const Tensor& in, const Tensor& out) {
+  const int R = in.size(0), D = in.size(1);
+  TORCH_CHECK(out.numel() == (int64_t)R * D, "nt_transpose sizes");
+  ntxent_transpose(f32(in, "in"), f32w(out, "out"), R, D, cur_stream());
+}
+void check_nt(int R, int Ccols, int D, int col_offset, int n_local) {
+  TORCH_CHECK(R % 16 == 0 && Ccols % 16 == 0, "ntxent: rows/cols must be multiples of 16");
+  TORCH_CHECK(D == 32 || D == 64 || D == 128 || D == 256, "ntxent: D must be 32/64/128/256");
+  TORCH_CHECK(2 * n_local == R, "ntxent: R must be 2*n_local");
+  TORCH_CHECK(col_offset >= 0 && col_offset + R <= Ccols, "ntxent: bad col_offset");
+}
+int64_t nt_fwd_splits(int64_t R, int64_t C) { return ntxent_fwd_splits(R, C); }
+int64_t nt_bwd_splits(int64_t nown, int64_t npart) { return ntxent_bwd_splits(nown, npart); }
+void nt_forward(const Tensor& znT, int64_t R, int64_t col_offset, int64_t n_local, double inv_temp,
+                const Tensor& part, int64_t splits, const Tensor& lse, const Tensor& loss) {
+  const int D = znT.size(0), Ccols = znT.size(1);
+  check_nt(R, Ccols, D, col_offset, n_local);
+  TORCH_CHECK(part.numel() >= splits * R * 3 && lse.numel() == R && loss.numel() == R,
+              "nt_forward sizes");
+  ntxent_forward(f32(znT, "znT"), R, Ccols, D, col_offset, n_local, (float)inv_temp,
+                 f32w(part, "part"), splits, f32w(lse, "lse"), f32w(loss, "loss"), cur_stream());
+}
+void nt_backward_part(bool row_mode, const Tensor& zn, const Tensor& znT, const Tensor& lse,
+                      int64_t R, int64_t col_offset, int64_t n_local, double inv_temp,
+                      double gscale, const c10::optional<Tensor>& gout, const Tensor& part,
+                      int64_t splits, const Tensor& out) {
+  const int D = znT.size(0), Ccols = znT.size(1);
+  check_nt(R, Ccols, D, col_offset, n_local);
+  TORCH_CHECK(zn.numel() == (int64_t)Ccols * D, "nt_backward: zn size");
+  const int64_t nown = row_mode ? R : Ccols;
+  TORCH_CHECK(part.numel() >= splits * nown * D && out.numel() == nown * D, "nt_backward sizes");
+  ntxent_backward_part(row_mode ? 1 : 0, f32(zn, "zn"), f32(znT, "znT"), f32(lse, "lse"), R, Ccols,
+                       D, col_offset, n_local, (float)inv_temp, (float)gscale, optf32(gout, "gout"),
+                       f32w(part, "part"), splits, f32w(out, "out"), cur_stream());
+}
+void nt_normalize_backward(const Tensor& zn, const Tensor& inv_norm, const Tensor& dzn,
+                           const c10::optional<Tensor>& dz_bf16, const c10::optional<Tensor>& dz_f32) {
+  const int R = zn.size(0), D = zn.size(1);
+  TORCH_CHECK(dzn.numel() == (int64_t)R * D, "nt_normalize_backward sizes");
+  ntxent_normalize_backward(f32(zn, "zn"), f32(inv_norm, "inv_norm"), f32(dzn, "dzn"), R, D,
+                            optbfw(dz_bf16, "dz_bf16"), optf32w(dz_f32, "dz_f32"), cur_stream());
+}
+void nt_reduce_loss(const Tensor& loss_rows, double scale, const Tensor& out) {
+  ntxent_reduce_loss(f32(loss_rows, "loss_rows"), loss_rows.numel(), (float)scale, f32w(out, "out"),
+                     cur_stream());
+}
+
+// ------------------------------------------------------------------------------- lars
+void lars_norms_op(const Tensor& p, const Tensor& g, const Tensor& chunk_beg,
+                   const Tensor& chunk_end, double grad_scale, const Tensor& norms) {
+  const int nchunks = chunk_beg.numel();
+  TORCH_CHECK(norms.numel() >= 2 * nchunks && p.numel() == g.numel(), "lars_norms sizes");
+  lars_norms(f32(p, "p"), f32(g, "g"), i32(chunk_beg, "chunk_beg"), i32(chunk_end, "chunk_end"),
+             nchunks, (float)grad_scale, f32w(norms, "norms"), cur_stream());
+}
+void lars_update_op(const Tensor& p, const Tensor& g, const Tensor& mom,
+                    const c10::optional<Tensor>& shadow, const Tensor& chunk_seg,
+                    const Tensor& chunk_beg, const Tensor& chunk_end, const Tensor& seg_chunk_beg,
+                    const Tensor& seg_chunk_end, const Tensor& seg_wd, const Tensor& seg_flags,
+                    const Tensor& norms, const Tensor& lr, double momentum, double trust, double eps,
+                    double grad_scale, bool nesterov) {
+  const int nchunks = chunk_beg.numel();
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == mom.numel(), "lars_update sizes");
+  if (shadow.has_value() && shadow->defined())
+    TORCH_CHECK(shadow->numel() == p.numel(), "lars_update: shadow size");
+  lars_update(f32w(p, "p"), f32(g, "g"), f32w(mom, "mom"), optbfw(shadow, "shadow"),
+              i32(chunk_seg, "chunk_seg"), i32(chunk_beg, "chunk_beg"), i32(chunk_end, "chunk_end"),
+              nchunks, i32(seg_chunk_beg, "seg_chunk_beg"), i32(seg_chunk_end, "seg_chunk_end"),
+              f32(seg_wd, "seg_wd"), i32(seg_flags, "seg_flags"), f32(norms, "norms"),
+              f32(lr, "lr"), (float)momentum, (float)trust, (float)eps, (float)grad_scale,
+              nesterov ? 1 : 0, cur_stream());
+}
+void lr_step_op(const Tensor& step, const Tensor& lr, double lr0, int64_t warmup, int64_t total,
+                int64_t mode) {
+  check_dev(step, at::kLong, "step");
+  lr_schedule_step(step.data_ptr<int64_t>(), f32w(lr, "lr"), lr0, warmup, total, (int)mode,
+                   cur_stream());
+}
+
+// ------------------------------------------------------------------------------- augment
+void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int64_t n,
+                int64_t views, int64_t OH, int64_t OW, int64_t Cpad, double strength, int64_t seed,
+                int64_t counter, int64_t view_offset, int64_t flags, const Tensor& out,
+                const c10::optional<Tensor>& params) {
+  check_dev(images, at::kByte, "images");
+  TORCH_CHECK(images.dim() == 4 && images.size(3) == 3, "augment: images must be [N,H,W,3] uint8");
+  const int H = images.size(1), W = images.size(2);
+  TORCH_CHECK(Cpad >= 3, "augment: Cpad >= 3");
+  TORCH_CHECK(out.numel() == views * n * OH * OW * Cpad, "augment: out size");
+  const int64_t* idx = nullptr;
+  if (indices.has_value() && indices->defined()) {
+    check_dev(*indices, at::kLong, "indices");
+    TORCH_CHECK(indices->numel() >= n, "augment: indices size");
+    idx = indices->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(n <= images.size(0), "augment: n > dataset");
+  }
+  if (!(flags & 1)) TORCH_CHECK(OH == H && OW == W, "augment: plain mode needs OH==H, OW==W");
+  float* po = nullptr;
+  if (params.has_value() && params->defined()) {
+    TORCH_CHECK(params->numel() >= views * n * 16, "augment: params size");
+    po = f32w(*params, "params");
+  }
+  simclr_augment(images.data_ptr<uint8_t>(), idx, n, views, H, W, OH, OW, Cpad, (float)strength,
+                 (uint64_t)seed, (uint64_t)counter, view_offset, flags, bfw(out, "out"), po,
+                 cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(simclr_amd, m) {
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom) -> ()", &igemm);
+  m.def("igemm_bm(int N) -> int", &igemm_bm);
+  m.def("wgrad_splits(int[] geom) -> int", &wgrad_nsplit);
+  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta) -> ()", &wgrad);
+  m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);
+  m.def("bn_blocks(int R, int C, int S) -> int", &bn_blocks);
+  m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
+  m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
+  m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt) -> ()", &bn_final);
+  m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
+  m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);
+  m.def("bn_bwd_reduce(Tensor dy, Tensor? y, Tensor x, Tensor mi, int S, bool relu, Tensor(a!) partial) -> ()", &bn_bwd_reduce_op);
+  m.def("bn_bwd_finalize(Tensor sums, Tensor mi, Tensor? gamma, int S, int C, float count, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!) coef) -> ()", &bn_bwd_final);
+  m.def("bn_bwd_apply(Tensor dy, Tensor? y, Tensor x, Tensor coef, int S, bool relu, Tensor(a!) dx, Tensor(b!)? dres) -> ()", &bn_bwd_apply_op);
+  m.def("avgpool_fwd(Tensor x, Tensor(a!) y, int Nb, int HW, int C) -> ()", &avgpool_fwd_op);
+  m.def("avgpool_bwd(Tensor dy, Tensor(a!) dx, int Nb, int HW, int C) -> ()", &avgpool_bwd_op);
+  m.def("colsum(Tensor x, Tensor(a!) out, float beta) -> ()", &colsum_op);
+  m.def("cast_to_bf16(Tensor x, Tensor(a!) y) -> ()", &cast_to_bf16);
+  m.def("cast_to_f32(Tensor x, Tensor(a!) y) -> ()", &cast_to_f32);
+  m.def("nt_normalize(Tensor z, Tensor(a!) zn, Tensor(b!) inv_norm) -> ()", &nt_normalize);
+  m.def("nt_transpose(Tensor x, Tensor(a!) out) -> ()", &nt_transpose);
+  m.def("nt_fwd_splits(int R, int C) -> int", &nt_fwd_splits);
+  m.def("nt_bwd_splits(int nown, int npart) -> int", &nt_bwd_splits);
+  m.def("nt_forward(Tensor znT, int R, int col_offset, int n_local, float inv_temp, Tensor(a!) part, int splits, Tensor(b!) lse, Tensor(c!) loss) -> ()", &nt_forward);
+  m.def("nt_backward_part(bool row_mode, Tensor zn, Tensor znT, Tensor lse, int R, int col_offset, int n_local, float inv_temp, float gscale, Tensor? gout, Tensor(a!) part, int splits, Tensor(b!) out) -> ()", &nt_backward_part);
+  m.def("nt_normalize_backward(Tensor zn, Tensor inv_norm, Tensor dzn, Tensor(a!)? dz_bf16, Tensor(b!)? dz_f32) -> ()", &nt_normalize_backward);
+  m.def("nt_reduce_loss(Tensor loss_rows, float scale, Tensor(a!) out) -> ()", &nt_reduce_loss);
+  m.def("lars_norms(Tensor p, Tensor g, Tensor chunk_beg, Tensor chunk_end, float grad_scale, Tensor(a!) norms) -> ()", &lars_norms_op);
+  m.def("lars_update(Tensor(a!) p, Tensor g, Tensor(b!) mom, Tensor(c!)? shadow, Tensor chunk_seg, Tensor chunk_beg, Tensor chunk_end, Tensor seg_chunk_beg, Tensor seg_chunk_end, Tensor seg_wd, Tensor seg_flags, Tensor norms, Tensor lr, float momentum, float trust, float eps, float grad_scale, bool nesterov) -> ()", &lars_update_op);
+  m.def("lr_step(Tensor(a!) step, Tensor(b!) lr, float lr0, int warmup, int total, int mode) -> ()", &lr_step_op);
+  m.def("augment(Tensor images, Tensor? indices, int n, int views, int OH, int OW, int Cpad, float strength, int seed, int counter, int view_offset, int flags, Tensor(a!) out, Tensor(b!)? params) -> ()", &augment_op);
+}

@@ -1,0 +1,442 @@
+// Segmented (per-view) cross-replica BatchNorm for bf16 NHWC activations on gfx950.
+//
+// Replaces SyncBatchNorm's batch_norm_stats / gather_stats_with_counts / batch_norm_elemt and
+// the backward_reduce / backward_elemt pair (torch/nn/modules/_functions.py:39-170) that the
+// reference runs once per view per layer (/root/reference/main.py:112-113,176).
+// Layout: x is [R, C] (R = S segments x Rs rows, C % 8 == 0), 16-byte vector accesses,
+// per-thread fixed channel chunk so scale/shift live in registers, fp32 math, deterministic
+// two-level reductions (block partials, then one reduce pass) — no float atomics.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// partial layout: [S][nblk][2][C]
+__global__ __launch_bounds__(256) void k_bn_stats(const uint16_t* __restrict__ x, int Rs, int C,
+                                                  int nblk, float* __restrict__ partial) {
+  const int TPR = C / 8 < 256 ? C / 8 : 256;
+  const int RPB = 256 / TPR;
+  const int seg = blockIdx.y;
+  const int blk = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int cchunk0 = tid % TPR;
+  const int rlane = tid / TPR;
+  __shared__ float red[256 * 2 * 8 / 8 * 8];  // [RPB][C chunk of this pass][2]
+  const int rows_per_blk = (Rs + nblk - 1) / nblk;
+  const int rbeg = blk * rows_per_blk;
+  const int rend = min(Rs, rbeg + rows_per_blk);
+  const uint16_t* xs = x + (size_t)seg * Rs * C;
+  for (int cc = cchunk0; cc < C / 8; cc += TPR) {
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+    if (rlane < RPB) {
+      for (int r = rbeg + rlane; r < rend; r += RPB) {
+        const u32x4 v = *(const u32x4*)(xs + (size_t)r * C + cc * 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = lo_bf(v[e]), b = hi_bf(v[e]);
+          s1[2 * e] += a; s2[2 * e] += a * a;
+          s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
+        }
+      }
+    }
+    // reduce over RPB row lanes through LDS: red[rlane][cchunk][e][2]
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[((rlane * TPR + cchunk0) * 8 + e) * 2 + 0] = s1[e];
+      red[((rlane * TPR + cchunk0) * 8 + e) * 2 + 1] = s2[e];
+    }
+    __syncthreads();
+    // TPR*8 channels handled in this pass; threads cover them
+    for (int t = tid; t < TPR * 8; t += 256) {
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < RPB; ++r) {
+        a += red[(r * TPR * 8 + t) * 2 + 0];
+        b += red[(r * TPR * 8 + t) * 2 + 1];
+      }
+      const int c = (cc - cchunk0) * 8 + t;  // channel base of this pass + t
+      float* dst = partial + (((size_t)seg * nblk + blk) * 2) * C;
+      dst[c] = a;
+      dst[C + c] = b;
+    }
+  }
+}
+
+__global__ void k_reduce_partials(const float* __restrict__ partial, int nblk, int S, int C,
+                                  float* __restrict__ stats) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over S*C
+  if (idx >= S * C) return;
+  const int s = idx / C, c = idx % C;
+  float a = 0.f, b = 0.f;
+  const float* src = partial + (size_t)s * nblk * 2 * C;
+  for (int i = 0; i < nblk; ++i) {
+    a += src[(size_t)i * 2 * C + c];
+    b += src[(size_t)i * 2 * C + C + c];
+  }
+  stats[(size_t)s * C + c] = a;           // [2][S][C]
+  stats[(size_t)S * C + s * C + c] = b;
+}
+
+// stats [2][S][C] -> mean_invstd [2][S][C]; sequential running-stat updates per segment
+__global__ void k_bn_finalize(const float* __restrict__ stats, int S, int C, float count, float eps,
+                              float momentum, float* running_mean, float* running_var,
+                              float* __restrict__ mi, int64_t* nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt != nullptr) nbt[0] += S;  // num_batches_tracked: one per view
+  if (c >= C) return;
+  float rm = running_mean ? running_mean[c] : 0.f;
+  float rv = running_var ? running_var[c] : 0.f;
+  const float unbias = count > 1.f ? count / (count - 1.f) : 1.f;
+  for (int s = 0; s < S; ++s) {
+    const float mean = stats[s * C + c] / count;
+    float var = stats[S * C + s * C + c] / count - mean * mean;
+    var = var > 0.f ? var : 0.f;
+    mi[s * C + c] = mean;
+    mi[S * C + s * C + c] = rsqrtf(var + eps);
+    rm = (1.f - momentum) * rm + momentum * mean;
+    rv = (1.f - momentum) * rv + momentum * var * unbias;
+  }
+  if (running_mean) running_mean[c] = rm;
+  if (running_var) running_var[c] = rv;
+}
+
+__global__ __launch_bounds__(256) void k_bn_apply(const uint16_t* __restrict__ x,
+                                                  const uint16_t* __restrict__ res,
+                                                  uint16_t* __restrict__ y,
+                                                  const float* __restrict__ mi,
+                                                  const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, int R, int C,
+                                                  int S, int relu) {
+  const int CH = C / 8;
+  const int TPR = CH < 256 ? CH : 256;
+  const int RPB = 256 / TPR;
+  const int Rs = R / S;
+  const int cc0 = threadIdx.x % TPR;
+  const int rl = threadIdx.x / TPR;
+  if (rl >= RPB) return;
+  for (int cc = cc0; cc < CH; cc += TPR) {
+    float sc[8], sh[8];
+    int seg_cached = -1;
+    for (int r = blockIdx.x * RPB + rl; r < R; r += gridDim.x * RPB) {
+      const int seg = r / Rs;
+      if (seg != seg_cached) {
+        seg_cached = seg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = cc * 8 + e;
+          const float mean = mi[seg * C + c], inv = mi[S * C + seg * C + c];
+          const float g = gamma ? gamma[c] : 1.f;
+          const float b = beta ? beta[c] : 0.f;
+          sc[e] = g * inv;
+          sh[e] = b - mean * g * inv;
+        }
+      }
+      const size_t off = (size_t)r * C + cc * 8;
+      const u32x4 v = *(const u32x4*)(x + off);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[2 * e] = lo_bf(v[e]) * sc[2 * e] + sh[2 * e];
+        o[2 * e + 1] = hi_bf(v[e]) * sc[2 * e + 1] + sh[2 * e + 1];
+      }
+      if (res) {
+        const u32x4 rv = *(const u32x4*)(res + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[2 * e] += lo_bf(rv[e]);
+          o[2 * e + 1] += hi_bf(rv[e]);
+        }
+      }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], 0.f);
+      }
+      u32x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = pack2bf(o[2 * e], o[2 * e + 1]);
+      *(u32x4*)(y + off) = w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bn_apply_eval(const uint16_t* __restrict__ x,
+                                                       const uint16_t* __restrict__ res,
+                                                       uint16_t* __restrict__ y,
+                                                       const float* __restrict__ rmean,
+                                                       const float* __restrict__ rvar,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps,
+                                                       int R, int C, int relu) {
+  const int CH = C / 8;
+  const size_t total = (size_t)R * CH;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CH);
+    const u32x4 v = *(const u32x4*)(x + i * 8);
+    u32x4 rv = {0, 0, 0, 0};
+    if (res) rv = *(const u32x4*)(res + i * 8);
+    u32x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float o2[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = cc * 8 + 2 * e + h;
+        const float inv = rsqrtf(rvar[c] + eps);
+        const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+        float xv = h ? hi_bf(v[e]) : lo_bf(v[e]);
+        float o = (xv - rmean[c]) * inv * g + b;
+        if (res) o += h ? hi_bf(rv[e]) : lo_bf(rv[e]);
+        if (relu) o = fmaxf(o, 0.f);
+        o2[h] = o;
+      }
+      w[e] = pack2bf(o2[0], o2[1]);
+    }
+    *(u32x4*)(y + i * 8) = w;
+  }
+}
+
+// Σg and Σg·x̂ partials, g = dy * (y > 0 if relu). partial layout [S][nblk][2][C]
+__global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint16_t* __restrict__ dy,
+                                                       const uint16_t* __restrict__ y,
+                                                       const uint16_t* __restrict__ x,
+                                                       const float* __restrict__ mi, int Rs,
+                                                       int C, int S, int relu, int nblk,
+                                                       float* __restrict__ partial) {
+  const int TPR = C / 8 < 256 ? C / 8 : 256;
+  const int RPB = 256 / TPR;
+  const int seg = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
+  const int cchunk0 = tid % TPR, rlane = tid / TPR;
+  __shared__ float red[256 * 2 * 8];
+  const int rows_per_blk = (Rs + nblk - 1) / nblk;
+  const int rbeg = blk * rows_per_blk;
+  const int rend = min(Rs, rbeg + rows_per_blk);
+  const size_t base = (size_t)seg * Rs * C;
+  for (int cc = cchunk0; cc < C / 8; cc += TPR) {
+    float s1[8], s2[8], mean[8], inv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = 0.f; s2[e] = 0.f;
+      mean[e] = mi[seg * C + cc * 8 + e];
+      inv[e] = mi[S * C + seg * C + cc * 8 + e];
+    }
+    if (rlane < RPB) {
+      for (int r = rbeg + rlane; r < rend; r += RPB) {
+        const size_t off = base + (size_t)r * C + cc * 8;
+        const u32x4 vd = *(const u32x4*)(dy + off);
+        const u32x4 vx = *(const u32x4*)(x + off);
+        u32x4 vy = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+        if (relu) vy = *(const u32x4*)(y + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = 2 * e + h;
+            float g = h ? hi_bf(vd[e]) : lo_bf(vd[e]);
+            if (relu) {
+              const float yy = h ? hi_bf(vy[e]) : lo_bf(vy[e]);
+              g = yy > 0.f ? g : 0.f;
+            }
+            const float xh = ((h ? hi_bf(vx[e]) : lo_bf(vx[e])) - mean[k]) * inv[k];
+            s1[k] += g;
+            s2[k] += g * xh;
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[((rlane * TPR + cchunk0) * 8 + e) * 2 + 0] = s1[e];
+      red[((rlane * TPR + cchunk0) * 8 + e) * 2 + 1] = s2[e];
+    }
+    __syncthreads();
+    for (int t = tid; t < TPR * 8; t += 256) {
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < RPB; ++r) {
+        a += red[(r * TPR * 8 + t) * 2 + 0];
+        b += red[(r * TPR * 8 + t) * 2 + 1];
+      }
+      const int c = (cc - cchunk0) * 8 + t;
+      float* dst = partial + (((size_t)seg * nblk + blk) * 2) * C;
+      dst[c] = a;
+      dst[C + c] = b;
+    }
+  }
+}
+
+// sums [2][S][C] (Σg, Σg·x̂, already all-reduced) -> dγ, dβ (summed over segments) and
+// coef [3][S][C] with dx = A·g + B·x + D
+__global__ void k_bn_bwd_finalize(const float* __restrict__ sums, const float* __restrict__ mi,
+                                  const float* __restrict__ gamma, int S, int C, float count,
+                                  float* dgamma, float* dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float dg = 0.f, db = 0.f;
+  const float gm = gamma ? gamma[c] : 1.f;
+  for (int s = 0; s < S; ++s) {
+    const float sg = sums[s * C + c], sgx = sums[S * C + s * C + c];
+    db += sg;
+    dg += sgx;
+    const float mean = mi[s * C + c], inv = mi[S * C + s * C + c];
+    const float A = gm * inv;
+    const float b = sg / count, c2 = sgx / count;
+    coef[s * C + c] = A;
+    coef[S * C + s * C + c] = -A * c2 * inv;
+    coef[2 * S * C + s * C + c] = -A * b + A * c2 * inv * mean;
+  }
+  if (dgamma) dgamma[c] = dg;
+  if (dbeta) dbeta[c] = db;
+}
+
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(const uint16_t* __restrict__ dy,
+                                                      const uint16_t* __restrict__ y,
+                                                      const uint16_t* __restrict__ x,
+                                                      const float* __restrict__ coef, int R,
+                                                      int C, int S, int relu,
+                                                      uint16_t* __restrict__ dx,
+                                                      uint16_t* __restrict__ dres) {
+  const int CH = C / 8;
+  const int TPR = CH < 256 ? CH : 256;
+  const int RPB = 256 / TPR;
+  const int Rs = R / S;
+  const int cc0 = threadIdx.x % TPR;
+  const int rl = threadIdx.x / TPR;
+  if (rl >= RPB) return;
+  for (int cc = cc0; cc < CH; cc += TPR) {
+    float A[8], B[8], D[8];
+    int seg_cached = -1;
+    for (int r = blockIdx.x * RPB + rl; r < R; r += gridDim.x * RPB) {
+      const int seg = r / Rs;
+      if (seg != seg_cached) {
+        seg_cached = seg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = cc * 8 + e;
+          A[e] = coef[seg * C + c];
+          B[e] = coef[S * C + seg * C + c];
+          D[e] = coef[2 * S * C + seg * C + c];
+        }
+      }
+      const size_t off = (size_t)r * C + cc * 8;
+      const u32x4 vd = *(const u32x4*)(dy + off);
+      const u32x4 vx = *(const u32x4*)(x + off);
+      u32x4 vy = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+      if (relu) vy = *(const u32x4*)(y + off);
+      u32x4 wdx, wg;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float o[2], gg[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * e + h;
+          float g = h ? hi_bf(vd[e]) : lo_bf(vd[e]);
+          if (relu) {
+            const float yy = h ? hi_bf(vy[e]) : lo_bf(vy[e]);
+            g = yy > 0.f ? g : 0.f;
+          }
+          const float xv = h ? hi_bf(vx[e]) : lo_bf(vx[e]);
+          o[h] = A[k] * g + B[k] * xv + D[k];
+          gg[h] = g;
+        }
+        wdx[e] = pack2bf(o[0], o[1]);
+        wg[e] = pack2bf(gg[0], gg[1]);
+      }
+      *(u32x4*)(dx + off) = wdx;
+      if (dres) *(u32x4*)(dres + off) = wg;
+    }
+  }
+}
+
+int apply_grid(int R, int C) {
+  const int CH = C / 8;
+  const int TPR = CH < 256 ? CH : 256;
+  const int RPB = 256 / TPR;
+  int blocks = (R + RPB - 1) / RPB;
+  // each thread should handle several rows for amortised scale/shift loads
+  blocks = (blocks + 7) / 8;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  return blocks;
+}
+
+}  // namespace
+
+int bn_stats_blocks_per_seg(int R, int C, int S) {
+  const int Rs = R / S;
+  const int CH = C / 8;
+  const int TPR = CH < 256 ? CH : 256;
+  const int RPB = 256 / TPR;
+  // aim for ~1024 blocks total with >= 8 row-iterations per thread
+  int nblk = 1024 / S;
+  const int max_blk = Rs / (RPB * 8);
+  if (nblk > max_blk) nblk = max_blk;
+  if (nblk < 1) nblk = 1;
+  return nblk;
+}
+
+void bn_stats_partial(const uint16_t* x, int R, int C, int S, float* partial, int* nblk_out,
+                      hipStream_t s) {
+  const int nblk = bn_stats_blocks_per_seg(R, C, S);
+  if (nblk_out) *nblk_out = nblk;
+  hipLaunchKernelGGL(k_bn_stats, dim3(nblk, S), dim3(256), 0, s, x, R / S, C, nblk, partial);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_reduce_partials(const float* partial, int nblk, int S, int C, float* stats, hipStream_t s) {
+  const int n = S * C;
+  hipLaunchKernelGGL(k_reduce_partials, dim3((n + 255) / 256), dim3(256), 0, s, partial, nblk, S, C,
+                     stats);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_finalize(const float* stats, int S, int C, float count, float eps, float momentum,
+                 float* running_mean, float* running_var, float* mean_invstd, int64_t* nbt,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, stats, S, C, count, eps,
+                     momentum, running_mean, running_var, mean_invstd, nbt);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* mi,
+              const float* gamma, const float* beta, int R, int C, int S, int relu,
+              hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_apply, dim3(apply_grid(R, C)), dim3(256), 0, s, x, res, y, mi, gamma,
+                     beta, R, C, S, relu);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_apply_eval(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* rmean,
+                   const float* rvar, const float* gamma, const float* beta, float eps, int R,
+                   int C, int relu, hipStream_t s) {
+  const size_t total = (size_t)R * (C / 8);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_bn_apply_eval, dim3(blocks), dim3(256), 0, s, x, res, y, rmean, rvar, gamma,
+                     beta, eps, R, C, relu);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mi, int R,
+                   int C, int S, int relu, float* partial, hipStream_t s) {
+  const int nblk = bn_stats_blocks_per_seg(R, C, S);
+  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk, S), dim3(256), 0, s, dy, y, x, mi, R / S, C, S,
+                     relu, nblk, partial);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_bwd_finalize(const float* sums, const float* mi, const float* gamma, int S, int C,
+                     float count, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, s, sums, mi, gamma, S,
+                     C, count, dgamma, dbeta, coef);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef,
+                  int R, int C, int S, int relu, uint16_t* dx, uint16_t* dres, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(apply_grid(R, C)), dim3(256), 0, s, dy, y, x, coef, R, C,
+                     S, relu, dx, dres);
+  HIP_CHECK_LAUNCH();
+}

@@ -1,0 +1,546 @@
+// Implicit-GEMM convolution engine for gfx950 (MI355X), bf16 NHWC, fp32 accumulation on MFMA.
+//
+// Replaces the implicit cuDNN/MIOpen convolutions of the reference's torchvision ResNet
+// (/root/reference/model.py:76-114).  Two kernels cover all three conv passes:
+//
+//   igemm_nt  C[M,N] = im2col(A)[M,K] · B[N,K]^T     forward  (B = weight, OHWI)
+//                                                    dgrad    (A = dY, B = flipped / parity-class
+//                                                              sub-kernel weight, see conv_hip.py)
+//             epilogue: + bias, bf16 NHWC store through LDS (16-B row stores, strided output
+//             mapping for stride-2 dgrad parity classes) and per-(segment, channel) Σx / Σx²
+//             partials for the following BatchNorm (saves the BN statistics read pass).
+//   wgrad_tn  dW[N,K] = Σ_m dY[m,N]^T · im2col(X)[m,K] split over m; both operands are staged
+//             row-major in LDS and read as MFMA fragments with ds_read_b64_tr_b16 (the transpose
+//             is free).  fp32 partial slabs are summed by wgrad_reduce straight into the flat fp32
+//             gradient buffer (OHWI = the im2col K order).
+//
+// Gather: the A operand is addressed per 16-byte chunk (8 channels) with raw buffer loads whose
+// out-of-range offset returns zeros, so conv padding / M and K tails need no branches around the
+// loads.  Tiles: BM x BN x 64, 256 threads (4 waves), mfma_f32_16x16x32_bf16, LDS double buffer
+// with an XOR chunk swizzle (cdna_hip_programming.md T2), XCD-aware block remap (T1).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+struct IgemmArgs {
+  const uint16_t* A;
+  const uint16_t* B;
+  uint16_t* out;
+  const float* bias;
+  float* stats;  // [gridM][2][N] partial Σx, Σx² (bf16-rounded outputs) or nullptr
+  int M, N, K;
+  int IH, IW, C;
+  int OH, OW, KW;
+  int ish, isw, dh, dw, ih0, iw0;
+  int OHp, OWp, osh, osw, ooh, oow, ldo;
+  int direct_out;
+  uint32_t a_bytes, b_bytes;
+  int nMb, nNb;
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int ACH = BM * 8 / 256;
+  constexpr int BCH = BN * 8 / 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* As = (uint16_t*)smem;          // [2][BM][64]
+  uint16_t* Bs = As + 2 * BM * 64;         // [2][BN][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mb = lbid / p.nNb, nb = lbid % p.nNb;
+  const int m0 = mb * BM, n0 = nb * BN;
+
+  const __amdgpu_buffer_rsrc_t ra_src =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb_src =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+
+  const int cch = tid & 7;
+  const int rbase = tid >> 3;
+  const int OHW = p.OH * p.OW;
+  int a_n[ACH], a_ih[ACH], a_iw[ACH];
+  bool a_ok[ACH];
+#pragma unroll
+  for (int j = 0; j < ACH; ++j) {
+    const int m = m0 + rbase + 32 * j;
+    a_ok[j] = m < p.M;
+    const int mm = a_ok[j] ? m : 0;
+    const int n = mm / OHW;
+    const int rem = mm - n * OHW;
+    const int oh = rem / p.OW;
+    const int ow = rem - oh * p.OW;
+    a_n[j] = n;
+    a_ih[j] = oh * p.ish + p.ih0;
+    a_iw[j] = ow * p.isw + p.iw0;
+  }
+  int b_off[BCH];
+  bool b_ok[BCH];
+#pragma unroll
+  for (int j = 0; j < BCH; ++j) {
+    const int nrow = n0 + rbase + 32 * j;
+    b_ok[j] = nrow < p.N;
+    b_off[j] = nrow * p.K;
+  }
+
+  u32x4 ra[ACH], rb[BCH];
+  const uint32_t OOB_A = p.a_bytes, OOB_B = p.b_bytes;
+
+  auto gload = [&](int kt) {
+    const int k = kt * 64 + cch * 8;
+    const bool kok = k < p.K;
+    const int tap = k / p.C;
+    const int ci = k - tap * p.C;
+    const int kh = tap / p.KW;
+    const int kw = tap - kh * p.KW;
+#pragma unroll
+    for (int j = 0; j < ACH; ++j) {
+      const int ih = a_ih[j] + kh * p.dh;
+      const int iw = a_iw[j] + kw * p.dw;
+      const bool ok = a_ok[j] && kok && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      const uint32_t off = ok ? (uint32_t)((((a_n[j] * p.IH + ih) * p.IW + iw) * p.C + ci) * 2) : OOB_A;
+      ra[j] = __builtin_amdgcn_raw_buffer_load_b128(ra_src, off, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      const uint32_t off = (b_ok[j] && kok) ? (uint32_t)((b_off[j] + k) * 2) : OOB_B;
+      rb[j] = __builtin_amdgcn_raw_buffer_load_b128(rb_src, off, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < ACH; ++j) {
+      const int row = rbase + 32 * j;
+      const int ch = cch ^ (row & 7);
+      *(u32x4*)(As + buf * BM * 64 + row * 64 + ch * 8) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      const int row = rbase + 32 * j;
+      const int ch = cch ^ (row & 7);
+      *(u32x4*)(Bs + buf * BN * 64 + row * 64 + ch * 8) = rb[j];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + 63) / 64;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const uint16_t* Ab = As + cur * BM * 64;
+    const uint16_t* Bb = Bs + cur * BN * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int row = wm * TM + fm * 16 + (lane & 15);
+        const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
+        af[fm] = *(const bf16x8*)(Ab + row * 64 + ch * 8);
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int row = wn * TN + fn * 16 + (lane & 15);
+        const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
+        bfr[fn] = *(const bf16x8*)(Bb + row * 64 + ch * 8);
+      }
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: bias, bf16 round, LDS-staged row stores, BN partial stats
+  constexpr int CST = BN + 8;  // padded row stride (elements)
+  uint16_t* Cs = (uint16_t*)smem;
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int col = wn * TN + fn * 16 + (lane & 15);
+    const float bv = (p.bias != nullptr && n0 + col < p.N) ? p.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * TM + fm * 16 + (lane >> 4) * 4 + i;
+        Cs[row * CST + col] = f2bf(acc[fm][fn][i] + bv);
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;            // 16-B chunks per row
+  constexpr int RSTEP = 256 / CPR;       // rows per pass
+  const int ch = tid % CPR;
+  const int r0 = tid / CPR;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const int n = n0 + ch * 8;
+  for (int row = r0; row < BM; row += RSTEP) {
+    const int m = m0 + row;
+    if (m >= p.M || n >= p.N) continue;
+    const u32x4 v = *(const u32x4*)(Cs + row * CST + ch * 8);
+    size_t o;
+    if (p.direct_out) {
+      o = (size_t)m * p.ldo + n;
+    } else {
+      const int img = m / OHW;
+      const int rem = m - img * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      o = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
+    }
+    *(u32x4*)(p.out + o) = v;
+    if (p.stats != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = lo_bf(v[e]), b = hi_bf(v[e]);
+        s1[2 * e] += a; s2[2 * e] += a * a;
+        s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
+      }
+    }
+  }
+  if (p.stats != nullptr) {
+    __syncthreads();
+    float* red = (float*)smem;  // [RSTEP][BN][2]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(r0 * BN + ch * 8 + e) * 2 + 0] = s1[e];
+      red[(r0 * BN + ch * 8 + e) * 2 + 1] = s2[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < p.N) {
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < RSTEP; ++r) {
+        a += red[(r * BN + tid) * 2 + 0];
+        b += red[(r * BN + tid) * 2 + 1];
+      }
+      p.stats[((size_t)mb * 2 + 0) * p.N + n0 + tid] = a;
+      p.stats[((size_t)mb * 2 + 1) * p.N + n0 + tid] = b;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------ wgrad
+struct WgradArgs {
+  const uint16_t* dY;  // [M][N] rows = forward output pixels
+  const uint16_t* X;   // forward input NHWC
+  float* partial;      // [splits][N][K]
+  int M, N, K;
+  int IH, IW, C;
+  int OH, OW, KW;
+  int ish, isw, dh, dw, ih0, iw0;
+  uint32_t dy_bytes, x_bytes;
+  int iters_per_split, splits, nCo, nKk;
+};
+
+template <int BCO, int BKK, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
+  constexpr int TCO = BCO / WM, TKK = BKK / WN;
+  constexpr int FM = TCO / 16, FN = TKK / 16;
+  constexpr int SD = BCO + 8;   // LDS row stride (elements) of the dY tile
+  constexpr int SX = BKK + 8;   // of the X tile
+  constexpr int CPD = BCO / 8, CPX = BKK / 8;
+  constexpr int DCH = 64 * CPD / 256, XCH = 64 * CPX / 256;
+  constexpr int RD = 256 / CPD, RX = 256 / CPX;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ds = (uint16_t*)smem;      // [2][64][SD]
+  uint16_t* Xs = Ds + 2 * 64 * SD;     // [2][64][SX]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = p.nCo * p.nKk;
+  const int split = lbid / tiles;
+  const int tile = lbid % tiles;
+  const int co0 = (tile / p.nKk) * BCO;
+  const int k0 = (tile % p.nKk) * BKK;
+
+  const __amdgpu_buffer_rsrc_t rd_src =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, (int)p.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx_src =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
+
+  // dY chunk owned by this thread
+  const int dch = tid % CPD, drow = tid / CPD;
+  const int dcol = co0 + dch * 8;
+  const bool dcol_ok = dcol < p.N;
+  // X chunk: fixed k per thread for the whole block
+  const int xch = tid % CPX, xrow = tid / CPX;
+  const int kk = k0 + xch * 8;
+  const bool k_ok = kk < p.K;
+  const int tap = k_ok ? kk / p.C : 0;
+  const int ci = kk - tap * p.C;
+  const int kh = tap / p.KW;
+  const int kw = tap - kh * p.KW;
+  const int OHW = p.OH * p.OW;
+
+  u32x4 rd[DCH], rx[XCH];
+  const int mbeg = split * p.iters_per_split * 64;
+  const int mend_raw = mbeg + p.iters_per_split * 64;
+  const int mend = mend_raw < p.M ? mend_raw : p.M;
+  const int nit = (mend - mbeg + 63) / 64;
+
+  auto gload = [&](int it) {
+    const int mb = mbeg + it * 64;
+#pragma unroll
+    for (int j = 0; j < DCH; ++j) {
+      const int m = mb + drow + RD * j;
+      const bool ok = m < mend && dcol_ok;
+      const uint32_t off = ok ? (uint32_t)(((size_t)m * p.N + dcol) * 2) : p.dy_bytes;
+      rd[j] = __builtin_amdgcn_raw_buffer_load_b128(rd_src, off, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < XCH; ++j) {
+      const int m = mb + xrow + RX * j;
+      bool ok = m < mend && k_ok;
+      const int mm = ok ? m : 0;
+      const int n = mm / OHW;
+      const int rem = mm - n * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      const int ih = oh * p.ish + p.ih0 + kh * p.dh;
+      const int iw = ow * p.isw + p.iw0 + kw * p.dw;
+      ok = ok && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      const uint32_t off = ok ? (uint32_t)((((n * p.IH + ih) * p.IW + iw) * p.C + ci) * 2) : p.x_bytes;
+      rx[j] = __builtin_amdgcn_raw_buffer_load_b128(rx_src, off, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < DCH; ++j)
+      *(u32x4*)(Ds + buf * 64 * SD + (drow + RD * j) * SD + dch * 8) = rd[j];
+#pragma unroll
+    for (int j = 0; j < XCH; ++j)
+      *(u32x4*)(Xs + buf * 64 * SX + (xrow + RX * j) * SX + xch * 8) = rx[j];
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  if (nit > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nit) gload(it + 1);
+    const uint16_t* Db = Ds + cur * 64 * SD;
+    const uint16_t* Xb = Xs + cur * 64 * SX;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r1 = ks * 32 + 8 * g + q;
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int col = wm * TCO + fm * 16 + 4 * pp;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Db + r1 * SD + col));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Db + (r1 + 4) * SD + col));
+        typedef short i16x8 __attribute__((ext_vector_type(8)));
+        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[fm] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int col = wn * TKK + fn * 16 + 4 * pp;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Xb + r1 * SX + col));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Xb + (r1 + 4) * SX + col));
+        typedef short i16x8 __attribute__((ext_vector_type(8)));
+        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[fn] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (it + 1 < nit) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* out = p.partial + (size_t)split * p.N * p.K;
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int kcol = k0 + wn * TKK + fn * 16 + li;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co0 + wm * TCO + fm * 16 + g * 4 + i;
+        if (co < p.N && kcol < p.K) out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
+      }
+    }
+}
+
+// out[co][tap][ci < Creal] (+)= Σ_s partial[s][co][tap*C + ci]
+__global__ void wgrad_reduce(const float* __restrict__ partial, float* __restrict__ out, int splits,
+                             int N, int K, int C, int Creal, float beta) {
+  const int taps = K / C;
+  const size_t total = (size_t)N * taps * Creal;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(idx % Creal);
+    const size_t t = idx / Creal;
+    const int tap = (int)(t % taps);
+    const int co = (int)(t / taps);
+    const size_t src = (size_t)co * K + tap * C + ci;
+    float s = 0.f;
+    for (int sp = 0; sp < splits; ++sp) s += partial[(size_t)sp * N * K + src];
+    out[idx] = beta != 0.f ? beta * out[idx] + s : s;
+  }
+}
+
+__global__ void wgrad_reduce_vec4(const float4* __restrict__ partial, float4* __restrict__ out,
+                                  int splits, size_t n4, float beta) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float4 s = partial[i];
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4 v = partial[(size_t)sp * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (beta != 0.f) {
+      const float4 o = out[i];
+      s.x += beta * o.x; s.y += beta * o.y; s.z += beta * o.z; s.w += beta * o.w;
+    }
+    out[i] = s;
+  }
+}
+
+// Wt[ci][khs][kws][co] = W[co][kh0 + khs*sh][kw0 + kws*sw][ci]   (bf16)
+__global__ void weight_transform(const uint16_t* __restrict__ W, uint16_t* __restrict__ Wt,
+                                 int Co, int KH, int KW, int Ci, int KHs, int KWs, int kh0, int sh,
+                                 int kw0, int sw) {
+  const size_t total = (size_t)Ci * KHs * KWs * Co;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int co = (int)(idx % Co);
+    size_t t = idx / Co;
+    const int kws = (int)(t % KWs);
+    t /= KWs;
+    const int khs = (int)(t % KHs);
+    const int ci = (int)(t / KHs);
+    const int kh = kh0 + khs * sh, kw = kw0 + kws * sw;
+    Wt[idx] = W[(((size_t)co * KH + kh) * KW + kw) * Ci + ci];
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_igemm(const IgemmArgs& a0, hipStream_t s) {
+  IgemmArgs a = a0;
+  a.nMb = (a.M + BM - 1) / BM;
+  a.nNb = (a.N + BN - 1) / BN;
+  const int grid = a.nMb * a.nNb;
+  size_t lds = (size_t)2 * (BM + BN) * 64 * 2;
+  const size_t cst = (size_t)BM * (BN + 8) * 2;
+  const size_t red = (size_t)(256 / (BN / 8)) * BN * 2 * 4;
+  if (cst > lds) lds = cst;
+  if (red > lds) lds = red;
+  hipLaunchKernelGGL((igemm_nt<BM, BN, WM, WN>), dim3(grid), dim3(256), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+int igemm_block_m(int N) { return N <= 64 ? 256 : 128; }
+
+void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
+                   uint16_t* out, const float* bias, float* stats, hipStream_t s) {
+  IgemmArgs a{};
+  a.A = A; a.B = B; a.out = out; a.bias = bias; a.stats = stats;
+  a.M = g.Nb * g.OH * g.OW; a.N = g.N; a.K = g.KH * g.KW * g.C;
+  a.IH = g.IH; a.IW = g.IW; a.C = g.C;
+  a.OH = g.OH; a.OW = g.OW; a.KW = g.KW;
+  a.ish = g.ish; a.isw = g.isw; a.dh = g.dh; a.dw = g.dw; a.ih0 = g.ih0; a.iw0 = g.iw0;
+  a.OHp = g.OHp; a.OWp = g.OWp; a.osh = g.osh; a.osw = g.osw; a.ooh = g.ooh; a.oow = g.oow;
+  a.ldo = g.ldo;
+  a.direct_out = (g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
+                  g.OWp == g.OW) ? 1 : 0;
+  a.a_bytes = (uint32_t)(a_elems * 2);
+  a.b_bytes = (uint32_t)((size_t)a.N * a.K * 2);
+  if (g.N <= 64) {
+    launch_igemm<256, 64, 4, 1>(a, s);
+  } else {
+    launch_igemm<128, 128, 2, 2>(a, s);
+  }
+}
+
+int wgrad_splits(const ConvGeom& g) {
+  const int M = g.Nb * g.OH * g.OW;
+  const int K = g.KH * g.KW * g.C;
+  const int tiles = ((g.N + 127) / 128) * ((K + 127) / 128);
+  const int iters = (M + 63) / 64;
+  int splits = (1024 + tiles - 1) / tiles;
+  int max_splits = iters / 8;
+  if (max_splits < 1) max_splits = 1;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  return splits;
+}
+
+void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
+                float* partial, int splits, float* out, int Creal, float beta, hipStream_t s) {
+  WgradArgs a{};
+  a.dY = dY; a.X = X; a.partial = partial;
+  a.M = g.Nb * g.OH * g.OW; a.N = g.N; a.K = g.KH * g.KW * g.C;
+  a.IH = g.IH; a.IW = g.IW; a.C = g.C;
+  a.OH = g.OH; a.OW = g.OW; a.KW = g.KW;
+  a.ish = g.ish; a.isw = g.isw; a.dh = g.dh; a.dw = g.dw; a.ih0 = g.ih0; a.iw0 = g.iw0;
+  a.dy_bytes = (uint32_t)((size_t)a.M * a.N * 2);
+  a.x_bytes = (uint32_t)(x_elems * 2);
+  const int iters = (a.M + 63) / 64;
+  a.splits = splits;
+  a.iters_per_split = (iters + splits - 1) / splits;
+  constexpr int BCO = 128, BKK = 128;
+  a.nCo = (a.N + BCO - 1) / BCO;
+  a.nKk = (a.K + BKK - 1) / BKK;
+  const int grid = a.nCo * a.nKk * splits;
+  const size_t lds = (size_t)2 * 64 * ((BCO + 8) + (BKK + 8)) * 2;
+  hipLaunchKernelGGL((wgrad_tn<BCO, BKK, 2, 2>), dim3(grid), dim3(256), lds, s, a);
+  HIP_CHECK_LAUNCH();
+  const int K = a.K;
+  if (Creal == g.C) {
+    const size_t n4 = (size_t)a.N * K / 4;
+    int blocks = (int)((n4 + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(wgrad_reduce_vec4, dim3(blocks), dim3(256), 0, s, (const float4*)partial,
+                       (float4*)out, splits, n4, beta);
+  } else {
+    const size_t total = (size_t)a.N * (K / g.C) * Creal;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, out, splits, a.N, K,
+                       g.C, Creal, beta);
+  }
+  HIP_CHECK_LAUNCH();
+}
+
+void conv_weight_transform(const uint16_t* W, uint16_t* Wt, int Co, int KH, int KW, int Ci,
+                           int KHs, int KWs, int kh0, int sh, int kw0, int sw, hipStream_t s) {
+  const size_t total = (size_t)Ci * KHs * KWs * Co;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(weight_transform, dim3(blocks), dim3(256), 0, s, W, Wt, Co, KH, KW, Ci, KHs,
+                     KWs, kh0, sh, kw0, sw);
+  HIP_CHECK_LAUNCH();
+}

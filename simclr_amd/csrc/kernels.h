@@ -1,0 +1,90 @@
+// Host-side launchers of the simclr_amd gfx950 kernels (raw pointers + stream; no torch types,
+// so the .hip translation units compile without the ATen headers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+// Conv geometry for the implicit GEMM (see conv.hip / conv_hip.py for the derivations).
+struct ConvGeom {
+  int Nb, IH, IW, C;        // gathered input tensor NHWC (C % 8 == 0)
+  int OH, OW;               // logical output grid (rows M = Nb*OH*OW)
+  int KH, KW;               // taps
+  int ish, isw, dh, dw;     // input = (oh*ish + kh*dh + ih0, ow*isw + kw*dw + iw0)
+  int ih0, iw0;
+  int N;                    // output channels (GEMM N)
+  int OHp, OWp, osh, osw, ooh, oow, ldo;  // physical output mapping
+};
+
+// ---- conv.hip
+int igemm_block_m(int N);
+void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
+                   uint16_t* out, const float* bias, float* stats, hipStream_t s);
+int wgrad_splits(const ConvGeom& g);
+void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
+                float* partial, int splits, float* out, int Creal, float beta, hipStream_t s);
+void conv_weight_transform(const uint16_t* W, uint16_t* Wt, int Co, int KH, int KW, int Ci,
+                           int KHs, int KWs, int kh0, int sh, int kw0, int sw, hipStream_t s);
+
+// ---- bn.hip  (x: [R, C] bf16 rows, S segments of R/S rows each)
+void bn_stats_partial(const uint16_t* x, int R, int C, int S, float* partial, int* nblk_per_seg,
+                      hipStream_t s);
+int bn_stats_blocks_per_seg(int R, int C, int S);
+void bn_reduce_partials(const float* partial, int nblk_per_seg, int S, int C, float* stats,
+                        hipStream_t s);
+void bn_finalize(const float* stats, int S, int C, float count, float eps, float momentum,
+                 float* running_mean, float* running_var, float* mean_invstd, int64_t* nbt,
+                 hipStream_t s);
+void bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* mean_invstd,
+              const float* gamma, const float* beta, int R, int C, int S, int relu,
+              hipStream_t s);
+void bn_apply_eval(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* rmean,
+                   const float* rvar, const float* gamma, const float* beta, float eps, int R,
+                   int C, int relu, hipStream_t s);
+void bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x,
+                   const float* mean_invstd, int R, int C, int S, int relu, float* partial,
+                   hipStream_t s);
+void bn_bwd_finalize(const float* sums, const float* mean_invstd, const float* gamma, int S, int C,
+                     float count, float* dgamma, float* dbeta, float* coef, hipStream_t s);
+void bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef,
+                  int R, int C, int S, int relu, uint16_t* dx, uint16_t* dres, hipStream_t s);
+
+// ---- misc.hip
+void avgpool_fwd(const uint16_t* x, uint16_t* y, int Nb, int HW, int C, hipStream_t s);
+void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int Nb, int HW, int C, hipStream_t s);
+void colsum_bf16(const uint16_t* x, int R, int C, float* out, float beta, hipStream_t s);
+void cast_f32_bf16(const float* x, uint16_t* y, size_t n, hipStream_t s);
+void cast_bf16_f32(const uint16_t* x, float* y, size_t n, hipStream_t s);
+
+// ---- ntxent.hip  (exact fp32 on v_mfma_f32_16x16x4_f32)
+void ntxent_normalize_f32(const uint16_t* z, int R, int D, float* zn, float* inv_norm,
+                          hipStream_t s);
+void ntxent_transpose(const float* in, float* out, int R, int D, hipStream_t s);
+int ntxent_fwd_splits(int R, int Ccols);
+int ntxent_bwd_splits(int nown, int npart);
+void ntxent_forward(const float* znT, int R, int Ccols, int D, int col_offset, int n_local,
+                    float inv_temp, float* part, int splits, float* lse, float* loss,
+                    hipStream_t s);
+void ntxent_backward_part(int row_mode, const float* zn, const float* znT, const float* lse, int R,
+                          int Ccols, int D, int col_offset, int n_local, float inv_temp,
+                          float gscale, const float* gout, float* part, int splits, float* out,
+                          hipStream_t s);
+void ntxent_normalize_backward(const float* zn, const float* inv_norm, const float* dzn, int R,
+                               int D, uint16_t* dz_bf16, float* dz_f32, hipStream_t s);
+void ntxent_reduce_loss(const float* loss_rows, int R, float scale, float* out, hipStream_t s);
+
+// ---- lars.hip (flat fp32 master / grad / momentum, bf16 shadow; per-segment table)
+void lars_norms(const float* p, const float* g, const int* chunk_beg, const int* chunk_end,
+                int nchunks, float grad_scale, float* norms, hipStream_t s);
+void lars_update(float* p, const float* g, float* mom, uint16_t* shadow, const int* chunk_seg,
+                 const int* chunk_beg, const int* chunk_end, int nchunks, const int* seg_chunk_beg,
+                 const int* seg_chunk_end, const float* seg_wd, const int* seg_flags,
+                 const float* norms, const float* lr_ptr, float momentum, float trust, float eps,
+                 float grad_scale, int nesterov, hipStream_t s);
+void lr_schedule_step(int64_t* step, float* lr_out, double lr0, int64_t warmup, int64_t total,
+                      int mode, hipStream_t s);
+
+// ---- augment.hip
+void simclr_augment(const uint8_t* images, const int64_t* indices, int n, int views, int H, int W,
+                    int OH, int OW, int Cpad, float strength, uint64_t seed, uint64_t counter,
+                    int view_offset, int flags, uint16_t* out, float* params_out, hipStream_t s);

@@ -1,0 +1,130 @@
+"""Datasets: CIFAR-10/100 readers (no torchvision) and a deterministic synthetic generator.
+
+Reference: ``torchvision.datasets.CIFAR10/100(root="~/pytorch_datasets", download=True)``
+(``/root/reference/main.py:156-167``, eval.py:213-244).  There is no network here, so the reader
+only loads data that is already on disk, from either the "python" pickled batches
+(``cifar-10-batches-py`` / ``cifar-100-python``) or the binary release
+(``cifar-10-batches-bin``); with ``synthetic=True`` (or when nothing is on disk and the caller
+allows it) a synthetic dataset of the same shape is generated.
+
+All datasets are returned as uint8 NHWC images + int64 labels so the whole training split can be
+uploaded to HBM once (CIFAR-10: 150 MB) and augmented on device.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+import torch
+
+DEFAULT_ROOT = "~/pytorch_datasets"
+
+
+@dataclass
+class ImageDataset:
+    images: np.ndarray   # uint8 [N, H, W, 3]
+    labels: np.ndarray   # int64 [N]
+    num_classes: int
+    name: str
+    synthetic: bool = False
+
+    def __len__(self) -> int:
+        return len(self.labels)
+
+    @property
+    def data(self):  # torchvision attribute name used by the reference (main.py:74)
+        return self.images
+
+
+def _load_pickle(path: Path) -> dict:
+    with open(path, "rb") as f:
+        return pickle.load(f, encoding="bytes")  # user-provided dataset file (CIFAR format)
+
+
+def _cifar_py(root: Path, name: str, train: bool) -> Optional[ImageDataset]:
+    if name == "cifar10":
+        d = root / "cifar-10-batches-py"
+        files = [d / f"data_batch_{i}" for i in range(1, 6)] if train else [d / "test_batch"]
+        key, ncls = b"labels", 10
+    else:
+        d = root / "cifar-100-python"
+        files = [d / ("train" if train else "test")]
+        key, ncls = b"fine_labels", 100
+    if not all(f.exists() for f in files):
+        return None
+    xs, ys = [], []
+    for f in files:
+        e = _load_pickle(f)
+        xs.append(np.asarray(e[b"data"], dtype=np.uint8).reshape(-1, 3, 32, 32))
+        ys.append(np.asarray(e[key], dtype=np.int64))
+    x = np.concatenate(xs).transpose(0, 2, 3, 1).copy()
+    return ImageDataset(x, np.concatenate(ys), ncls, name)
+
+
+def _cifar_bin(root: Path, name: str, train: bool) -> Optional[ImageDataset]:
+    if name != "cifar10":
+        d = root / "cifar-100-binary"
+        files = [d / ("train.bin" if train else "test.bin")]
+        rec, lab_off, ncls = 3074, 1, 100
+    else:
+        d = root / "cifar-10-batches-bin"
+        files = ([d / f"data_batch_{i}.bin" for i in range(1, 6)] if train
+                 else [d / "test_batch.bin"])
+        rec, lab_off, ncls = 3073, 0, 10
+    if not all(f.exists() for f in files):
+        return None
+    raw = np.concatenate([np.fromfile(f, dtype=np.uint8) for f in files]).reshape(-1, rec)
+    labels = raw[:, lab_off].astype(np.int64)
+    x = raw[:, rec - 3072:].reshape(-1, 3, 32, 32).transpose(0, 2, 3, 1).copy()
+    return ImageDataset(x, labels, ncls, name)
+
+
+def synthetic_dataset(n: int, num_classes: int = 10, size: int = 32, seed: int = 0,
+                      name: str = "synthetic", template_seed: int = 1234) -> ImageDataset:
+    """Class-structured random images: per-class colour/frequency template + per-image noise,
+    so that learned features are non-trivially separable (used when no data is on disk)."""
+    g = np.random.default_rng(seed)
+    labels = g.integers(0, num_classes, size=n).astype(np.int64)
+    yy, xx = np.meshgrid(np.linspace(0, 1, size), np.linspace(0, 1, size), indexing="ij")
+    tmpl = np.empty((num_classes, size, size, 3), dtype=np.float32)
+    cg = np.random.default_rng(template_seed)  # shared by train and test splits
+    for c in range(num_classes):
+        col = cg.uniform(40, 215, size=3)
+        fy, fx = cg.uniform(1, 4, size=2)
+        ph = cg.uniform(0, 2 * np.pi)
+        pat = np.sin(2 * np.pi * (fy * yy + fx * xx) + ph)
+        tmpl[c] = col[None, None, :] + 35.0 * pat[..., None]
+    imgs = np.empty((n, size, size, 3), dtype=np.uint8)
+    bs = 4096
+    for s in range(0, n, bs):
+        e = min(n, s + bs)
+        noise = g.normal(0, 25.0, size=(e - s, size, size, 3)).astype(np.float32)
+        imgs[s:e] = np.clip(tmpl[labels[s:e]] + noise, 0, 255).astype(np.uint8)
+    return ImageDataset(imgs, labels, num_classes, name, synthetic=True)
+
+
+def load_dataset(name: str, train: bool = True, root: str = DEFAULT_ROOT,
+                 synthetic: bool = False, synthetic_size: Optional[int] = None,
+                 allow_synthetic_fallback: bool = False, seed: int = 0,
+                 image_size: int = 32) -> ImageDataset:
+    name = name.lower()
+    if name not in ("cifar10", "cifar100"):
+        raise ValueError("experiment.name must be cifar10 or cifar100, got {!r}".format(name))
+    ncls = 10 if name == "cifar10" else 100
+    if not synthetic:
+        r = Path(os.path.expanduser(root))
+        for reader in (_cifar_py, _cifar_bin):
+            ds = reader(r, name, train)
+            if ds is not None:
+                return ds
+        if not allow_synthetic_fallback:
+            raise FileNotFoundError(
+                f"{name} not found under {r} (no network to download it); "
+                "place the CIFAR python/binary batches there or run with data.synthetic=true")
+    n = synthetic_size if synthetic_size is not None else (50000 if train else 10000)
+    return synthetic_dataset(n, ncls, size=image_size, seed=seed + (0 if train else 7919),
+                             name=f"synthetic-{name}")

@@ -1,0 +1,150 @@
+"""NT-Xent loss (normalised temperature-scaled cross entropy).
+
+Reference API: ``NT_Xent(temperature, reduction, device)(view0, view1)``
+(``/root/reference/loss.py:4-65``).  Semantics: anchors are the 2N rows of both
+views; for each, the logits are cosine similarities / τ to every other row (self excluded), the
+target is the same image's other view; ``reduction="mean"`` averages over the 2N anchors,
+``"sum"`` sums, ``"none"`` returns a (2, N) tensor [view0 anchors; view1 anchors].
+
+Extension (north star): ``gather=True`` all-gathers ẑ from every rank over RCCL, so
+each anchor sees 2·N·W − 1 candidates instead of 2N − 1 (negatives from the global batch).  The
+gradient w.r.t. other ranks' columns flows back through an all-reduce of the column gradients.
+Parity default is ``gather=False`` (the reference's loss is per-GPU local).
+
+GPU path: the fused exact-fp32 MFMA kernels of ``csrc/ntxent.hip`` (no N×N logits, no mask or
+concat copies, no host→device target upload per call).  CPU / fp32 path: torch ops.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from torch import nn
+
+from ..ops import registry
+from ..parallel import state as pstate
+
+
+def nt_xent_torch(z: torch.Tensor, n: int, temperature: float, reduction: str = "mean",
+                  gather: bool = False, group=None, world_size: int = 1, rank: int = 0):
+    """Oracle implementation on torch ops; ``z`` = [view0; view1] of shape [2n, d]."""
+    zn = F.normalize(z.float(), p=2, dim=1)
+    R = zn.shape[0]
+    if gather and world_size > 1:
+        from torch.distributed.nn.functional import all_gather
+        cols = torch.cat(all_gather(zn, group=group), dim=0)
+        col_offset = rank * R
+    else:
+        cols = zn
+        col_offset = 0
+    sim = zn @ cols.t() / temperature
+    idx = torch.arange(R, device=z.device)
+    self_mask = torch.zeros_like(sim, dtype=torch.bool)
+    self_mask[idx, col_offset + idx] = True
+    sim = sim.masked_fill(self_mask, float("-inf"))
+    targets = col_offset + torch.where(idx < n, idx + n, idx - n)
+    rows = F.cross_entropy(sim, targets, reduction="none")
+    if reduction == "none":
+        return rows.view(2, n)
+    if reduction == "sum":
+        return rows.sum()
+    return rows.sum() / n * 0.5
+
+
+class _NTXentHipFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, n, temperature, reduction, gather, st):
+        from ..ops import _ext
+        ops = _ext.ops()
+        R, D = z.shape
+        dev = z.device
+        zb = z.contiguous() if z.dtype == torch.bfloat16 else z.to(torch.bfloat16).contiguous()
+        zn = torch.empty((R, D), device=dev, dtype=torch.float32)
+        inv = torch.empty((R,), device=dev, dtype=torch.float32)
+        ops.nt_normalize(zb, zn, inv)
+        if gather and st.world_size > 1:
+            zall = torch.empty((st.world_size * R, D), device=dev, dtype=torch.float32)
+            dist.all_gather_into_tensor(zall, zn, group=st.group)
+            col_offset = st.rank * R
+        else:
+            zall = zn
+            col_offset = 0
+        Ccols = zall.shape[0]
+        znT = torch.empty((D, Ccols), device=dev, dtype=torch.float32)
+        ops.nt_transpose(zall, znT)
+        splits = ops.nt_fwd_splits(R, Ccols)
+        part = torch.empty((splits * R * 3,), device=dev, dtype=torch.float32)
+        lse = torch.empty((R,), device=dev, dtype=torch.float32)
+        rows = torch.empty((R,), device=dev, dtype=torch.float32)
+        inv_t = 1.0 / temperature
+        ops.nt_forward(znT, R, col_offset, n, inv_t, part, splits, lse, rows)
+        out = torch.empty((1,), device=dev, dtype=torch.float32)
+        scale = 1.0 / R if reduction == "mean" else 1.0
+        ops.nt_reduce_loss(rows, scale, out)
+        ctx.save_for_backward(zn, zall, znT, lse, inv)
+        ctx.cfg = (n, inv_t, scale, col_offset, gather, st, z.dtype)
+        return out.view(())
+
+    @staticmethod
+    def backward(ctx, gout):
+        from ..ops import _ext
+        ops = _ext.ops()
+        zn, zall, znT, lse, inv = ctx.saved_tensors
+        n, inv_t, scale, col_offset, gather, st, zdtype = ctx.cfg
+        R, D = zn.shape
+        Ccols = zall.shape[0]
+        dev = zn.device
+        g = gout.reshape(1).float().contiguous()
+        s_row = ops.nt_bwd_splits(R, Ccols)
+        part = torch.empty((s_row * R * D,), device=dev, dtype=torch.float32)
+        d_rows = torch.empty((R, D), device=dev, dtype=torch.float32)
+        ops.nt_backward_part(True, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part, s_row,
+                             d_rows)
+        s_col = ops.nt_bwd_splits(Ccols, R)
+        part2 = torch.empty((s_col * Ccols * D,), device=dev, dtype=torch.float32)
+        d_cols = torch.empty((Ccols, D), device=dev, dtype=torch.float32)
+        ops.nt_backward_part(False, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part2,
+                             s_col, d_cols)
+        if gather and st.world_size > 1:
+            dist.all_reduce(d_cols, group=st.group)
+        d_rows += d_cols[col_offset:col_offset + R]
+        if zdtype == torch.bfloat16:
+            dz = torch.empty((R, D), device=dev, dtype=torch.bfloat16)
+            ops.nt_normalize_backward(zn, inv, d_rows, dz, None)
+        else:
+            dz = torch.empty((R, D), device=dev, dtype=torch.float32)
+            ops.nt_normalize_backward(zn, inv, d_rows, None, dz)
+        return dz, None, None, None, None, None
+
+
+class NTXent(nn.Module):
+    def __init__(self, temperature: float = 0.1, reduction: str = "mean",
+                 device: Optional[torch.device] = None, gather: bool = False):
+        assert temperature > 0.0
+        assert reduction in {"none", "mean", "sum"}
+        super().__init__()
+        self.temperature = temperature
+        self.reduction = reduction
+        self.gather = gather
+
+    def forward(self, view0: torch.Tensor, view1: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``forward(view0, view1)`` as the reference, or ``forward(z)`` with z = [view0; view1]."""
+        if view1 is not None:
+            z = torch.cat([view0, view1], dim=0)
+            n = view0.shape[0]
+        else:
+            z = view0
+            n = z.shape[0] // 2
+        st = pstate.get()
+        R, D = z.shape
+        if (z.is_cuda and self.reduction != "none" and registry.use_hip(z) and R % 16 == 0
+                and D in (32, 64, 128, 256)):
+            return _NTXentHipFn.apply(z, n, self.temperature, self.reduction, self.gather, st)
+        return nt_xent_torch(z, n, self.temperature, self.reduction, self.gather, st.group,
+                             st.world_size, st.rank)
+
+
+# reference class name
+NT_Xent = NTXent

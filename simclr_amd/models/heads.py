@@ -1,0 +1,116 @@
+"""Projection head and downstream classifiers.
+
+Parity: ``ProjectionHead`` (``/root/reference/model.py:56-73``), ``LinearClassifier``
+(model.py:7-21), ``CentroidClassifier`` (model.py:24-53).  ``NonLinearClassifier`` is imported
+by the reference's eval.py (eval.py:16,304) but never defined; it is
+implemented here as Linear(F,F) → BN1d → ReLU → Linear(F,C), mirroring the projection head
+(an inferred design, documented as such).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from ..ops.batchnorm import BatchNorm1d
+from ..ops.conv import effective_weight
+
+
+class Linear(nn.Linear):
+    """``nn.Linear`` with the bf16-shadow / flat-gradient plumbing of ``ops.conv``.
+
+    ``emit_bn_stats``: the GEMM epilogue also emits the statistics partials for a following
+    BatchNorm1d (true for ``linear1`` of the heads)."""
+
+    emit_bn_stats = False
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops import linear as linear_ops
+        return linear_ops.linear_module(self, x)
+
+
+class _MLP(nn.Module):
+    """Linear → BN1d → ReLU → Linear with the fused BN+ReLU epilogue."""
+
+    def __init__(self, in_features: int, hidden: int, out_features: int, last_bias: bool,
+                 attr: str):
+        super().__init__()
+        lin1 = Linear(in_features, hidden)
+        lin1.emit_bn_stats = True
+        seq = nn.Sequential(OrderedDict([
+            ("linear1", lin1),
+            ("bn1", BatchNorm1d(hidden)),
+            ("relu1", nn.ReLU()),
+            ("linear2", Linear(hidden, out_features, bias=last_bias)),
+        ]))
+        self._attr = attr
+        setattr(self, attr, seq)
+
+    @property
+    def _seq(self) -> nn.Sequential:
+        return getattr(self, self._attr)
+
+    def forward(self, x: torch.Tensor, segments: int = 1) -> torch.Tensor:
+        s = self._seq
+        h = s.linear1(x)
+        h = s.bn1(h, relu=True, segments=segments)
+        return s.linear2(h)
+
+    @property
+    def in_features(self) -> int:
+        return self._seq.linear1.in_features
+
+    @property
+    def out_features(self) -> int:
+        return self._seq.linear2.out_features
+
+
+class ProjectionHead(_MLP):
+    """g(h) = W2 · ReLU(BN(W1 h + b1)); keys ``projection_head.{linear1,bn1,linear2}.*``."""
+
+    def __init__(self, num_last_hidden_units: int, d: int):
+        super().__init__(num_last_hidden_units, num_last_hidden_units, d, last_bias=False,
+                         attr="projection_head")
+
+
+class NonLinearClassifier(_MLP):
+    def __init__(self, num_features: int = 128, num_classes: int = 10):
+        super().__init__(num_features, num_features, num_classes, last_bias=True,
+                         attr="classifier")
+
+
+class LinearClassifier(nn.Module):
+    def __init__(self, num_features: int = 128, num_classes: int = 10):
+        super().__init__()
+        self.classifier = nn.Linear(num_features, num_classes)
+
+    def forward(self, inputs: torch.Tensor, segments: int = 1) -> torch.Tensor:
+        return self.classifier(inputs)
+
+
+class CentroidClassifier(nn.Module):
+    """Dot-product against per-class mean features (unnormalised, model.py:24-53)."""
+
+    def __init__(self, weights: torch.Tensor):
+        super().__init__()
+        self.weights = weights  # d x num_classes
+
+    def forward(self, inputs: torch.Tensor, segments: int = 1) -> torch.Tensor:
+        return torch.matmul(inputs.to(self.weights.dtype), self.weights)
+
+    @staticmethod
+    def create_weights(dataset, num_classes: int) -> torch.Tensor:
+        """Per-class means as one segmented reduction (index_add) instead of C masked means."""
+        X = dataset.data
+        Y = dataset.targets.to(X.device).long()
+        sums = torch.zeros(num_classes, X.shape[1], dtype=torch.float64, device=X.device)
+        sums.index_add_(0, Y, X.double())
+        counts = torch.bincount(Y, minlength=num_classes).clamp_min(1).to(sums.dtype)
+        means = (sums / counts[:, None]).to(X.dtype)
+        # classes with no samples give NaN in the reference (mean of empty); keep that contract
+        empty = torch.bincount(Y, minlength=num_classes) == 0
+        if bool(empty.any()):
+            means[empty] = float("nan")
+        return means.t().contiguous()  # d x num_classes

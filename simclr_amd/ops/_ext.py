@@ -1,0 +1,59 @@
+"""Loader for the in-tree HIP extension ``simclr_amd/_C.so`` (built by ``simclr_amd.csrc.build``).
+
+The library is loaded with ``torch.ops.load_library`` (plain dlopen of the in-tree file — never a
+site-packages or JIT-cache copy) and registers ``torch.ops.simclr_amd.*``.  On a GPU tensor an op
+that needs the library raises if it is missing instead of silently running torch ops.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_LIB = Path(__file__).resolve().parent.parent / "_C.so"
+_lock = threading.Lock()
+_loaded = False
+_error: Exception | None = None
+
+
+def lib_path() -> Path:
+    return _LIB
+
+
+def load(build_if_missing: bool = False) -> bool:
+    global _loaded, _error
+    if _loaded:
+        return True
+    with _lock:
+        if _loaded:
+            return True
+        if not _LIB.exists() and build_if_missing:
+            from ..csrc import build as _b
+            _b.build()
+        if not _LIB.exists():
+            _error = FileNotFoundError(
+                f"{_LIB} not found; build it with `python -m simclr_amd.csrc.build`")
+            return False
+        try:
+            torch.ops.load_library(str(_LIB))
+            _loaded = True
+        except Exception as e:  # pragma: no cover - surfaced by require()
+            _error = e
+            return False
+    return True
+
+
+def available() -> bool:
+    return load(build_if_missing=False)
+
+
+def require() -> None:
+    if not load(build_if_missing=os.environ.get("SIMCLR_AUTOBUILD", "1") == "1"):
+        raise RuntimeError(f"simclr_amd HIP extension unavailable: {_error}")
+
+
+def ops():
+    require()
+    return torch.ops.simclr_amd

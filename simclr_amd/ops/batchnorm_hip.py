@@ -1,0 +1,129 @@
+"""Autograd wrapper of the segmented SyncBN kernels (``csrc/bn.hip``).
+
+Per layer and step: forward = [stats partials from the producing conv's epilogue, or a stats
+pass] → reduce → (one all-reduce of [Σx; Σx²] for all views when distributed) → finalize
+(mean/invstd, running stats, num_batches_tracked += views) → fused apply (affine + residual +
+ReLU).  Backward = reduce (Σg, Σg·x̂ with the ReLU mask) → (one all-reduce) → finalize (dγ, dβ
+written straight into the flat fp32 gradient buffer) → fused apply (dx, and d(residual) = g).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _ext
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[R, C] contiguous row view of a channels_last 4-D or a 2-D tensor."""
+    if t.dim() == 4:
+        if not t.is_contiguous(memory_format=torch.channels_last):
+            t = t.contiguous(memory_format=torch.channels_last)
+        return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+    return t.contiguous()
+
+
+def _empty_like_cl(x: torch.Tensor) -> torch.Tensor:
+    if x.dim() == 4:
+        return torch.empty(x.shape, device=x.device, dtype=x.dtype,
+                           memory_format=torch.channels_last)
+    return torch.empty_like(x)
+
+
+def _allreduce(t: torch.Tensor, st) -> None:
+    if st.world_size > 1:
+        dist.all_reduce(t, group=st.group)
+
+
+def _grad_out(param: torch.Tensor):
+    slot = getattr(param, "_slot", None)
+    if slot is not None:
+        return slot.grad, slot
+    return torch.empty(param.shape, device=param.device, dtype=torch.float32), None
+
+
+class BatchNormHipFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, bn, segments, relu, st):
+        ops = _ext.ops()
+        S = segments
+        C = x.shape[1]
+        xr = _rows(x)
+        R = xr.shape[0]
+        dev = x.device
+        stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        pre = getattr(x, "_simclr_stats", None)
+        if pre is not None and pre[1] % S == 0:
+            partial, nblk_total = pre
+            ops.bn_reduce(partial, nblk_total // S, S, C, stats)
+        else:
+            nblk = ops.bn_blocks(R, C, S)
+            partial = torch.empty((S * nblk * 2 * C,), device=dev, dtype=torch.float32)
+            ops.bn_stats(xr, S, partial)
+            ops.bn_reduce(partial, nblk, S, C, stats)
+        _allreduce(stats, st)
+        count = float((R // S) * st.world_size)
+        mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean, bn.running_var,
+                        mi, bn.num_batches_tracked)
+        y = _empty_like_cl(x)
+        res_r = _rows(residual) if residual is not None else None
+        ops.bn_apply(xr, res_r, _rows(y), mi, weight.detach(), bias.detach(), S, relu)
+        ctx.save_for_backward(x, y if relu else None, mi, weight)
+        ctx.cfg = (S, relu, residual is not None, count, st)
+        ctx.bias = bias
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ops = _ext.ops()
+        x, y, mi, weight = ctx.saved_tensors
+        S, relu, has_res, count, st = ctx.cfg
+        C = x.shape[1]
+        xr = _rows(x)
+        R = xr.shape[0]
+        dev = x.device
+        dyr = _rows(dy)
+        if dyr.dtype != torch.bfloat16:
+            dyr = dyr.to(torch.bfloat16)
+        yr = _rows(y) if y is not None else None
+        nblk = ops.bn_blocks(R, C, S)
+        partial = torch.empty((S * nblk * 2 * C,), device=dev, dtype=torch.float32)
+        ops.bn_bwd_reduce(dyr, yr, xr, mi, S, relu, partial)
+        sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        ops.bn_reduce(partial, nblk, S, C, sums)
+        _allreduce(sums, st)
+        dgamma, gslot = _grad_out(weight)
+        dbeta, bslot = _grad_out(ctx.bias)
+        coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
+        ops.bn_bwd_finalize(sums, mi, weight.detach(), S, C, count, dgamma, dbeta, coef)
+        if gslot is not None:
+            gslot.store.mark_ready(gslot.index)
+        if bslot is not None:
+            bslot.store.mark_ready(bslot.index)
+        dx = _empty_like_cl(x)
+        dres = _empty_like_cl(x) if has_res else None
+        ops.bn_bwd_apply(dyr, yr, xr, coef, S, relu, _rows(dx),
+                         _rows(dres) if dres is not None else None)
+        gw = None if gslot is not None else dgamma
+        gb = None if bslot is not None else dbeta
+        return dx, gw, gb, dres, None, None, None, None
+
+
+def batch_norm_train(x, bn, segments, residual, relu, st):
+    if x.shape[1] % 8 != 0:
+        raise ValueError(f"HIP BatchNorm needs channels % 8 == 0, got {x.shape[1]}")
+    if residual is not None and residual.dtype != x.dtype:
+        residual = residual.to(x.dtype)
+    return BatchNormHipFn.apply(x, bn.weight, bn.bias, residual, bn, segments, relu, st)
+
+
+def batch_norm_eval(x, bn, residual, relu):
+    ops = _ext.ops()
+    y = _empty_like_cl(x)
+    ops.bn_apply_eval(_rows(x), _rows(residual) if residual is not None else None, _rows(y),
+                      bn.running_mean, bn.running_var, bn.weight.detach(), bn.bias.detach(),
+                      bn.eps, relu)
+    return y

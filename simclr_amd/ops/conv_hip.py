@@ -1,0 +1,172 @@
+"""Autograd wrapper of the implicit-GEMM conv kernels (``csrc/conv.hip``).
+
+Tensors: activations are logical NCHW / physical NHWC (``channels_last``) bf16; weights are
+consumed as OHWI bf16 (the flat store's shadow) and their gradients are produced as OHWI fp32
+directly into the flat gradient buffer.
+
+Pass decomposition (all on ``igemm_nt`` / ``wgrad_tn``):
+
+* forward   : gather x with (stride s, pad p); epilogue also emits per-channel Σy, Σy² block
+              partials that the following BatchNorm consumes instead of re-reading y.
+* dgrad s=1 : dx = conv(dy, flip(W)ᵀ) — gather dy with offset −(K−1−p), B = weight_transform
+              (W[co][K−1−kh][K−1−kw][ci] → [ci][kh][kw][co]).
+* dgrad s=2 : per output parity class (r, c) ∈ {0,1}²: the taps kh ≡ r+p (mod 2) form a
+              stride-1 sub-convolution with negative tap step (dh = −1) whose outputs land on
+              rows 2i+r, cols 2j+c (strided epilogue).  No zero-inserted MACs.
+* wgrad     : dW[co][kh][kw][ci] = Σ_m dy[m][co] · im2col(x)[m][(kh,kw,ci)], split over m.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _ext
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    """Contiguous NHWC view of a channels_last 4-D tensor (copies only if needed)."""
+    if t.dim() == 4:
+        if not t.is_contiguous(memory_format=torch.channels_last):
+            t = t.contiguous(memory_format=torch.channels_last)
+        return t.permute(0, 2, 3, 1)
+    return t.contiguous()
+
+
+def _empty_cl(n, c, h, w, device, dtype=torch.bfloat16):
+    return torch.empty((n, c, h, w), device=device, dtype=dtype,
+                       memory_format=torch.channels_last)
+
+
+def fwd_geom(N, H, W, C, OH, OW, KH, KW, stride, pad, Co):
+    return [N, H, W, C, OH, OW, KH, KW, stride, stride, 1, 1, -pad, -pad, Co,
+            OH, OW, 1, 1, 0, 0, Co]
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def shadow_ohwi(weight: torch.Tensor, cpad: int) -> torch.Tensor:
+    """bf16 OHWI weight for the kernels (flat-store shadow when bound; cast otherwise)."""
+    slot = getattr(weight, "_slot", None)
+    if slot is not None and slot.shadow is not None:
+        w = slot.shadow  # [Co, KH, KW, Ci] bf16 contiguous
+    else:
+        w = weight.detach().permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+    ci = w.shape[-1]
+    if cpad != ci:
+        w = torch.nn.functional.pad(w, (0, cpad - ci)).contiguous()
+    return w
+
+
+class ConvHipFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, weight: torch.Tensor, stride: int, pad: int,
+                emit_stats: bool):
+        ops = _ext.ops()
+        N, Cx, H, W = x.shape
+        Co, Ci, KH, KW = weight.shape
+        assert Cx >= Ci and Cx % 8 == 0, f"input channels {Cx} vs weight {Ci}"
+        OH = (H + 2 * pad - KH) // stride + 1
+        OW = (W + 2 * pad - KW) // stride + 1
+        xn = _nhwc(x)
+        w = shadow_ohwi(weight, Cx)
+        y = _empty_cl(N, Co, OH, OW, x.device)
+        g = fwd_geom(N, H, W, Cx, OH, OW, KH, KW, stride, pad, Co)
+        stats = None
+        M = N * OH * OW
+        bm = ops.igemm_bm(Co)
+        if emit_stats and M % bm == 0:
+            stats = torch.empty(((M // bm) * 2 * Co,), device=x.device, dtype=torch.float32)
+        ops.igemm(xn, w, y.permute(0, 2, 3, 1), None, stats, g)
+        if stats is not None:
+            y._simclr_stats = (stats, M // bm)  # consumed by the next BatchNorm
+        ctx.save_for_backward(x, weight)
+        ctx.geom = (N, H, W, Cx, Ci, OH, OW, KH, KW, stride, pad, Co)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy: torch.Tensor):
+        ops = _ext.ops()
+        x, weight = ctx.saved_tensors
+        N, H, W, Cx, Ci, OH, OW, KH, KW, stride, pad, Co = ctx.geom
+        dyn = _nhwc(dy)
+        if dyn.dtype != torch.bfloat16:
+            dyn = dyn.to(torch.bfloat16)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            assert Cx == Ci, "dgrad through a channel-padded stem is not supported"
+            w = shadow_ohwi(weight, Ci)
+            dx = conv_dgrad(ops, dyn, w, N, H, W, Ci, OH, OW, KH, KW, stride, pad, Co)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            g = fwd_geom(N, H, W, Cx, OH, OW, KH, KW, stride, pad, Co)
+            splits = ops.wgrad_splits(g)
+            K = KH * KW * Cx
+            partial = torch.empty((splits * Co * K,), device=dy.device, dtype=torch.float32)
+            slot = getattr(weight, "_slot", None)
+            if slot is not None:
+                out = slot.grad  # [Co, KH, KW, Ci] fp32 contiguous view into the flat buffer
+            else:
+                out = torch.empty((Co, KH, KW, Ci), device=dy.device, dtype=torch.float32)
+            ops.wgrad(dyn, _nhwc(x), partial, out, g, splits, Ci, 0.0)
+            if slot is not None:
+                slot.store.mark_ready(slot.index)
+            else:
+                dw = out.permute(0, 3, 1, 2)
+        return dx, dw, None, None, None
+
+
+_WT_CACHE: dict = {}
+
+
+def conv_dgrad(ops, dyn, w_ohwi, N, H, W, Ci, OH, OW, KH, KW, stride, pad, Co):
+    """dx [N, Ci, H, W] (channels_last) from dy (NHWC view) and the OHWI bf16 weight."""
+    dev = dyn.device
+    dx = _empty_cl(N, Ci, H, W, dev)
+    dxn = dx.permute(0, 2, 3, 1)
+    if stride == 1:
+        wt = torch.empty((Ci, KH, KW, Co), device=dev, dtype=torch.bfloat16)
+        ops.weight_transform(w_ohwi, wt, [Co, KH, KW, Ci, KH, KW, KH - 1, -1, KW - 1, -1])
+        g = [N, OH, OW, Co, H, W, KH, KW, 1, 1, 1, 1, -(KH - 1 - pad), -(KW - 1 - pad), Ci,
+             H, W, 1, 1, 0, 0, Ci]
+        ops.igemm(dyn, wt, dxn, None, None, g)
+        return dx
+    assert stride == 2, "only stride 1/2 convolutions are supported"
+    classes = []
+    for r in (0, 1):
+        for c in (0, 1):
+            kh0 = (r + pad) % 2
+            kw0 = (c + pad) % 2
+            nkh = (KH - kh0 + 1) // 2 if kh0 < KH else 0
+            nkw = (KW - kw0 + 1) // 2 if kw0 < KW else 0
+            ohc = (H - r + 1) // 2
+            owc = (W - c + 1) // 2
+            classes.append((r, c, kh0, kw0, nkh, nkw, ohc, owc))
+    if any(cl[4] == 0 or cl[5] == 0 for cl in classes if cl[6] > 0 and cl[7] > 0):
+        dx.zero_()
+    for (r, c, kh0, kw0, nkh, nkw, ohc, owc) in classes:
+        if nkh == 0 or nkw == 0 or ohc == 0 or owc == 0:
+            continue
+        wt = torch.empty((Ci, nkh, nkw, Co), device=dev, dtype=torch.bfloat16)
+        ops.weight_transform(w_ohwi, wt, [Co, KH, KW, Ci, nkh, nkw, kh0, 2, kw0, 2])
+        ih0 = (r + pad - kh0) // 2
+        iw0 = (c + pad - kw0) // 2
+        g = [N, OH, OW, Co, ohc, owc, nkh, nkw, 1, 1, -1, -1, ih0, iw0, Ci,
+             H, W, 2, 2, r, c, Ci]
+        ops.igemm(dyn, wt, dxn, None, None, g)
+    return dx
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride, padding, weight_param=None,
+           emit_stats: bool = True) -> Optional[torch.Tensor]:
+    """HIP conv forward; returns None if this configuration is not supported by the kernels."""
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    if sh != sw or ph != pw or sh not in (1, 2) or x.dtype != torch.bfloat16 or x.dim() != 4:
+        return None
+    if x.shape[1] % 8 != 0:
+        return None
+    param = weight_param if weight_param is not None else w
+    return ConvHipFn.apply(x, param, sh, ph, emit_stats)

@@ -1,0 +1,33 @@
+"""Global average pool (avgpool + flatten) on the HIP kernels of ``csrc/misc.hip``."""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+from .conv_hip import _nhwc
+
+
+class AvgPoolHipFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ops = _ext.ops()
+        N, C, H, W = x.shape
+        y = torch.empty((N, C), device=x.device, dtype=torch.bfloat16)
+        ops.avgpool_fwd(_nhwc(x), y, N, H * W, C)
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ops = _ext.ops()
+        N, C, H, W = ctx.shape
+        dx = torch.empty((N, C, H, W), device=dy.device, dtype=torch.bfloat16,
+                         memory_format=torch.channels_last)
+        ops.avgpool_bwd(dy.contiguous().to(torch.bfloat16), dx.permute(0, 2, 3, 1), N, H * W, C)
+        return dx
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    if x.dtype != torch.bfloat16 or x.shape[1] % 8 != 0:
+        return x.float().mean(dim=(2, 3)).to(x.dtype)
+    return AvgPoolHipFn.apply(x)

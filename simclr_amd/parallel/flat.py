@@ -1,0 +1,185 @@
+"""Flat parameter store + bucketed data-parallel gradient reducer.
+
+Reference: ``DistributedDataParallel(model, device_ids=[rank])`` with default 25 MiB buckets,
+``broadcast_buffers=True`` (``/root/reference/main.py:178``): per-parameter
+grads, bucket all-reduces overlapped with backward, averaged by 1/W, plus a broadcast of all BN
+buffers before *every* forward.
+
+MI355X design:
+
+* All trainable parameters live in ONE fp32 master buffer (``master``), with a parallel fp32
+  gradient buffer (``grad``), momentum buffer (owned by the optimizer) and bf16 shadow
+  (``shadow``) that the compute kernels read.  Conv weights are stored OHWI (the implicit-GEMM
+  K order), presented to PyTorch as OIHW-shaped ``channels_last`` views, so ``state_dict`` and
+  ``nn.Module`` semantics are unchanged.  Each parameter is 64-element (256 B) aligned.
+* The layout is in *reverse registration order* (≈ backward order), so gradient buckets are
+  contiguous slices that fill front to back during backward.  Kernels write gradients straight
+  into their slice (``ParamSlot``) and call ``mark_ready``; a full bucket is handed to RCCL on a
+  dedicated comm stream (``all_reduce`` SUM; the 1/W average is folded into the LARS kernel's
+  ``grad_scale``).  Buckets launch strictly in index order on every rank (RCCL requirement).
+* No per-forward buffer broadcast: with SyncBN every rank already holds identical running
+  statistics (the reference's per-forward broadcast is redundant traffic).
+* Bucket size: default 32 MiB; on MI355X the 7 xGMI links of a GPU give the ring ~7x one link,
+  so buckets of tens of MiB amortise RCCL's ~10-20 µs launch floor while the first bucket still
+  starts early in the backward (``first_bucket_mb`` smaller, like DDP's 1 MiB first bucket).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from ..ops.conv import ParamSlot
+from . import state as pstate
+
+ALIGN = 64
+
+
+def _is_conv_weight(p: torch.Tensor) -> bool:
+    return p.dim() == 4
+
+
+class FlatParamStore:
+    def __init__(self, model: nn.Module, device: torch.device, shadow_dtype=torch.bfloat16,
+                 bucket_mb: float = 32.0, first_bucket_mb: float = 4.0,
+                 group=None, world_size: Optional[int] = None):
+        self.model = model
+        self.device = torch.device(device)
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        named = list(reversed(named))  # ≈ backward order
+        self.names: List[str] = [n for n, _ in named]
+        self.params: List[nn.Parameter] = [p for _, p in named]
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.offsets = offs
+        self.total = off
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.shadow = (torch.zeros(self.total, dtype=shadow_dtype, device=self.device)
+                       if shadow_dtype is not None else None)
+        self.slots: List[ParamSlot] = []
+        for i, (p, o) in enumerate(zip(self.params, offs)):
+            n = p.numel()
+            src = p.detach().to(self.device, torch.float32)
+            if _is_conv_weight(p):
+                co, ci, kh, kw = p.shape
+                mview = self.master[o:o + n].view(co, kh, kw, ci)
+                mview.copy_(src.permute(0, 2, 3, 1))
+                p.data = mview.permute(0, 3, 1, 2)
+                gview = self.grad[o:o + n].view(co, kh, kw, ci)
+                p.grad = gview.permute(0, 3, 1, 2)
+                sview = self.shadow[o:o + n].view(co, kh, kw, ci) if self.shadow is not None else None
+            else:
+                mview = self.master[o:o + n].view(p.shape)
+                mview.copy_(src)
+                p.data = mview
+                gview = self.grad[o:o + n].view(p.shape)
+                p.grad = gview
+                sview = self.shadow[o:o + n].view(p.shape) if self.shadow is not None else None
+            slot = ParamSlot(sview, gview, i, self)
+            p._slot = slot
+            self.slots.append(slot)
+        self.refresh_shadow()
+        # ---- reducer
+        st = pstate.get()
+        self.group = group if group is not None else st.group
+        self.world_size = world_size if world_size is not None else st.world_size
+        self._build_buckets(bucket_mb, first_bucket_mb)
+        self._comm_stream = None
+        self._works: List = []
+        self.reset_step()
+
+    # ------------------------------------------------------------------ parameters
+    def refresh_shadow(self) -> None:
+        """Re-derive the bf16 shadow from the fp32 master (after init / checkpoint load)."""
+        if self.shadow is not None:
+            with torch.no_grad():
+                self.shadow.copy_(self.master)
+
+    def rebind(self) -> None:
+        """Re-point ``p.data``/``p.grad`` at the flat buffers (after load_state_dict copies)."""
+        for p, slot in zip(self.params, self.slots):
+            if p.grad is None or p.grad.data_ptr() != slot.grad.data_ptr():
+                p.grad = slot.grad.permute(0, 3, 1, 2) if slot.grad.dim() == 4 else slot.grad
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def segments(self) -> List[Tuple[int, int]]:
+        return [(o, p.numel()) for o, p in zip(self.offsets, self.params)]
+
+    # ------------------------------------------------------------------ reducer
+    def _build_buckets(self, bucket_mb: float, first_bucket_mb: float) -> None:
+        cap_first = int(first_bucket_mb * 1024 * 1024 / 4)
+        cap = int(bucket_mb * 1024 * 1024 / 4)
+        self.bucket_of: List[int] = []
+        self.buckets: List[Tuple[int, int, int]] = []  # (beg, end, n_params)
+        beg, count, size = 0, 0, 0
+        for i, p in enumerate(self.params):
+            limit = cap_first if not self.buckets else cap
+            n = (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+            if count > 0 and size + n > limit:
+                self.buckets.append((beg, self.offsets[i], count))
+                beg, count, size = self.offsets[i], 0, 0
+            self.bucket_of.append(len(self.buckets))
+            count += 1
+            size += n
+        if count > 0:
+            self.buckets.append((beg, self.total, count))
+
+    def reset_step(self) -> None:
+        self._ready = [0] * len(self.buckets)
+        self._seen = [False] * len(self.params)
+        self._next_launch = 0
+        self._works = []
+
+    def mark_ready(self, index: int) -> None:
+        if self.world_size <= 1 or self._seen[index]:
+            return
+        self._seen[index] = True
+        b = self.bucket_of[index]
+        self._ready[b] += 1
+        while (self._next_launch < len(self.buckets)
+               and self._ready[self._next_launch] == self.buckets[self._next_launch][2]):
+            self._launch(self._next_launch)
+            self._next_launch += 1
+
+    def _launch(self, b: int) -> None:
+        beg, end, _ = self.buckets[b]
+        view = self.grad[beg:end]
+        if view.is_cuda:
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(device=view.device)
+            cur = torch.cuda.current_stream(view.device)
+            self._comm_stream.wait_stream(cur)
+            with torch.cuda.stream(self._comm_stream):
+                work = dist.all_reduce(view, group=self.group, async_op=True)
+            self._works.append(work)
+        else:
+            self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def finish(self) -> None:
+        """Flush unlaunched buckets (unused params), then make the compute stream wait."""
+        if self.world_size <= 1:
+            return
+        while self._next_launch < len(self.buckets):
+            self._launch(self._next_launch)
+            self._next_launch += 1
+        for w in self._works:
+            w.wait()
+        if self._comm_stream is not None:
+            torch.cuda.current_stream(self.grad.device).wait_stream(self._comm_stream)
+        self.reset_step()
+
+    def broadcast_from(self, src: int = 0) -> None:
+        """Make all ranks start from rank ``src``'s parameters and buffers (DDP ctor semantics)."""
+        if self.world_size <= 1:
+            return
+        dist.broadcast(self.master, src=src, group=self.group)
+        for b in self.model.buffers():
+            dist.broadcast(b, src=src, group=self.group)
+        self.refresh_shadow()

@@ -1,0 +1,205 @@
+"""SimCLR contrastive pre-training (the ``main`` entry point).
+
+Reference: ``/root/reference/main.py:61-131,134-180`` (call stacks §3.1-3.2).  Per
+step the reference does warmup LR → zero_grad → two DDP forwards (view0, view1) → NT-Xent →
+backward (DDP bucket all-reduces, SyncBN collectives) → LARC.step → cosine step; once per epoch
+rank 0 logs ``Epoch:{e}/{E} progress:{p:.3f} loss:{l:.3f}, lr:{lr:.7f}`` (last batch's loss) and
+saves ``epoch={E}-{name}`` every ``save_model_epoch`` epochs.
+
+MI355X step (``Trainer.step``), identical math:
+  augment kernel (both views, on device) → ONE forward of the 2N batch with per-view BN
+  statistics (``segments=2``) on the implicit-GEMM / fused-BN kernels → fused NT-Xent →
+  backward with gradients written into the flat fp32 buffer and bucketed RCCL all-reduces on a
+  comm stream → ``lr_step`` + fused LARS (no host sync anywhere in the step).
+Optionally the whole step (fwd + bwd + optimizer) is captured once into a hipGraph and replayed
+(``runtime.hip_graph=true``) to remove per-kernel launch overhead.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..config import check_pretrain_conf
+from ..data.datasets import load_dataset
+from ..data.loader import ContrastiveLoader
+from ..loss.ntxent import NTXent
+from ..models.contrastive import ContrastiveModel
+from ..ops import registry
+from ..optim.lars import FusedLARS, weight_decay_per_param
+from ..optim.schedule import MODE_WARMUP_COSINE, calculate_initial_lr
+from ..parallel.flat import FlatParamStore
+from ..runtime.dist import init_distributed
+from ..utils.checkpoint import checkpoint_name, save_reference_checkpoint, save_resume, load_resume
+from ..utils.misc import cfg_get, seed_everything, MetricsWriter
+
+log = logging.getLogger(__name__)
+
+
+def build_contrastive_model(cfg, device, precision: str):
+    model = ContrastiveModel(base_cnn=cfg["experiment"]["base_cnn"], d=cfg["parameter"]["d"],
+                             cifar_stem=cfg_get(cfg, "model.cifar_stem", None),
+                             stem_padding=cfg_get(cfg, "model.stem_padding", 3))
+    model = model.to(device)
+    shadow = torch.bfloat16 if (precision == "bf16" and device.type == "cuda") else None
+    store = FlatParamStore(model, device, shadow_dtype=shadow,
+                           bucket_mb=cfg_get(cfg, "runtime.bucket_mb", 32.0))
+    store.broadcast_from(0)
+    return model, store
+
+
+class Trainer:
+    """Owns model, flat store, optimizer, loss and the (optionally graph-captured) step."""
+
+    def __init__(self, cfg, st, dataset_len: int, precision: Optional[str] = None):
+        self.cfg = cfg
+        self.st = st
+        self.device = st.device
+        prec = precision or cfg_get(cfg, "runtime.precision", "bf16")
+        self.precision = prec if self.device.type == "cuda" else "fp32"
+        self.model, self.store = build_contrastive_model(cfg, self.device, self.precision)
+        batches = cfg["experiment"]["batches"]
+        world = st.world_size
+        # reference: int(num_samples / (batches * world)) (main.py:76)
+        self.steps_per_epoch = max(1, int(dataset_len / (batches * world)))
+        self.total_steps = cfg["parameter"]["epochs"] * self.steps_per_epoch
+        self.warmup_steps = cfg["parameter"]["warmup_epochs"] * self.steps_per_epoch
+        wds = weight_decay_per_param(self.store, cfg["experiment"]["decay"])
+        self.opt = FusedLARS(self.store, wds, lr0=calculate_initial_lr(cfg),
+                             momentum=cfg["parameter"]["momentum"], nesterov=False,
+                             trust_coefficient=0.001, eps=1e-8, lars=True,
+                             schedule_mode=MODE_WARMUP_COSINE, warmup_steps=self.warmup_steps,
+                             total_steps=self.total_steps)
+        self.loss_fn = NTXent(temperature=cfg["parameter"]["temperature"],
+                              gather=bool(cfg_get(cfg, "loss.gather", False)))
+        self.hip = self.device.type == "cuda" and registry.use_hip(self.store.master) \
+            and self.precision == "bf16"
+        self.model.train()
+        self.graph = None
+        self._static_x = None
+        self._static_loss = None
+
+    def prepare(self, x: torch.Tensor) -> torch.Tensor:
+        if self.precision == "bf16" and self.device.type == "cuda":
+            return x
+        x = x.float()
+        if x.shape[1] != 3:
+            x = x[:, :3]
+        return x.contiguous()
+
+    def _step_body(self, x: torch.Tensor) -> torch.Tensor:
+        z = self.model(x, segments=2)
+        loss = self.loss_fn(z)
+        if not self.hip:
+            self.store.zero_grad()
+        loss.backward()
+        self.store.finish()
+        self.opt.step()
+        return loss.detach()
+
+    def step(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.prepare(x)
+        if self.graph is not None:
+            self._static_x.copy_(x)
+            self.graph.replay()
+            self.opt.host_step += 1
+            return self._static_loss
+        return self._step_body(x)
+
+    def capture(self, x: torch.Tensor, warmup: int = 2) -> None:
+        """Capture one full training step into a hipGraph (after ``warmup`` eager steps)."""
+        x = self.prepare(x)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_body(x)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._static_x = x.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._static_loss = self._step_body(self._static_x)
+        self.opt.host_step -= 1  # the captured body incremented it once; replays add per step
+        self.graph = g
+
+
+def pretrain(cfg) -> dict:
+    st = init_distributed(cfg, use_cuda=cfg["parameter"].get("use_cuda", True))
+    check_pretrain_conf(cfg)
+    registry.set_backend(cfg_get(cfg, "runtime.backend", "auto"))
+    seed = cfg["parameter"]["seed"]
+    seed_everything(seed, deterministic=bool(cfg_get(cfg, "runtime.deterministic", False)))
+    rank = st.rank
+    log.info("Using {}".format(st.device))
+    ds = load_dataset(cfg["experiment"]["name"], train=True,
+                      root=cfg_get(cfg, "data.root", "~/pytorch_datasets"),
+                      synthetic=bool(cfg_get(cfg, "data.synthetic", False)),
+                      synthetic_size=cfg_get(cfg, "data.synthetic_size", None),
+                      allow_synthetic_fallback=bool(cfg_get(cfg, "data.synthetic_fallback", False)),
+                      seed=seed)
+    loader = ContrastiveLoader(ds, cfg["experiment"]["batches"], st.device, rank=rank,
+                               world=st.world_size, strength=cfg["experiment"]["strength"],
+                               seed=seed, views=2)
+    tr = Trainer(cfg, st, len(ds))
+    epochs = cfg["parameter"]["epochs"]
+    start_epoch = 1
+    resume = cfg_get(cfg, "runtime.resume", None)
+    if resume:
+        blob = load_resume(resume, tr.model, tr.opt, tr.store)
+        start_epoch = int(blob["epoch"]) + 1
+        loader.counter = int(blob["step"])
+    max_steps = cfg_get(cfg, "runtime.max_steps", None)
+    use_graph = bool(cfg_get(cfg, "runtime.hip_graph", False)) and tr.hip
+    metrics = MetricsWriter("metrics.jsonl" if rank == 0 else None)
+    save_every = cfg["experiment"]["save_model_epoch"]
+    step_global = tr.opt.host_step
+    loss = torch.zeros(())
+    summary = {"epochs_run": 0, "steps": 0}
+    t_start = time.time()
+    done = False
+    for epoch in range(start_epoch, epochs + 1):
+        loader.set_epoch(epoch)
+        if st.device.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.time()
+        nsteps = 0
+        for x, _ in loader:
+            if use_graph and tr.graph is None:
+                tr.capture(x)
+            loss = tr.step(x)
+            nsteps += 1
+            step_global += 1
+            if max_steps is not None and step_global >= max_steps:
+                done = True
+                break
+        if st.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = max(time.time() - t0, 1e-9)
+        imgs = nsteps * cfg["experiment"]["batches"] * st.world_size
+        summary.update(epochs_run=summary["epochs_run"] + 1, steps=step_global)
+        if rank == 0:
+            lval = float(loss.item())
+            lr = tr.opt.logged_lr
+            logging.info("Epoch:{}/{} progress:{:.3f} loss:{:.3f}, lr:{:.7f}".format(
+                epoch, epochs, epoch / epochs, lval, lr))
+            metrics.write(epoch=epoch, step=step_global, loss=lval, lr=lr,
+                          images_per_sec=imgs / dt, seconds=dt)
+            summary.update(loss=lval, lr=lr, images_per_sec=imgs / dt)
+            if epoch % save_every == 0:
+                save_reference_checkpoint(tr.model, checkpoint_name(
+                    epoch, cfg["experiment"]["output_model_name"]))
+                if cfg_get(cfg, "runtime.save_resume", True):
+                    save_resume("resume-{}.pt".format(epoch), tr.model, tr.opt, epoch,
+                                loader.counter)
+        if done:
+            break
+    summary["wall_seconds"] = time.time() - t_start
+    metrics.close()
+    return summary

@@ -1,0 +1,97 @@
+"""Checkpoint I/O in the reference's format, plus resumable training state.
+
+Reference contract (``/root/reference/main.py:129-131``): rank 0 writes
+``torch.save(ddp_model.state_dict(), "epoch={E}-{output_model_name}")`` — an ``OrderedDict`` of
+fp32 NCHW/OIHW tensors with torchvision names and the DDP ``module.`` prefix (weights + BN
+buffers only).  Readers strip ``module.`` (eval.py:257) and load ``strict=False``.
+
+This module writes exactly that (contiguous fp32 CPU tensors, regardless of the internal OHWI /
+flat-buffer layout), and additionally a ``resume-<E>.pt`` with optimizer momentum, step, epoch
+and RNG state (an extension: the reference cannot resume).  Loading always uses
+``torch.load(..., weights_only=True)``.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from pathlib import Path
+from typing import Optional
+
+import torch
+from torch import nn
+
+PREFIX = "module."
+
+
+def reference_state_dict(model: nn.Module, prefix: str = PREFIX) -> "OrderedDict[str, torch.Tensor]":
+    out = OrderedDict()
+    for k, v in model.state_dict().items():
+        t = v.detach()
+        if t.is_floating_point():
+            t = t.float()
+        out[prefix + k] = t.contiguous().cpu().clone()
+    return out
+
+
+def save_reference_checkpoint(model: nn.Module, path: str) -> None:
+    torch.save(reference_state_dict(model), path)
+
+
+def checkpoint_name(epoch: int, output_model_name: str) -> str:
+    return "epoch={}-{}".format(epoch, output_model_name)
+
+
+def strip_prefix(sd: dict, prefix: str = PREFIX) -> dict:
+    return {(k[len(prefix):] if k.startswith(prefix) else k): v for k, v in sd.items()}
+
+
+def load_state(path, map_location="cpu") -> dict:
+    return torch.load(path, map_location=map_location, weights_only=True)
+
+
+@torch.no_grad()
+def load_into(model: nn.Module, path, strict: bool = False, store=None):
+    """Load a reference-format checkpoint (prefix stripped) into ``model`` in place, keeping the
+    flat-store views intact (copy_ into existing tensors, never rebind)."""
+    sd = strip_prefix(load_state(path))
+    own = model.state_dict(keep_vars=True)
+    missing, unexpected = [], []
+    for k, v in sd.items():
+        if k not in own:
+            unexpected.append(k)
+            continue
+        tgt = own[k]
+        tgt.data.copy_(v.to(tgt.device, tgt.dtype).reshape(tgt.shape))
+    for k in own:
+        if k not in sd:
+            missing.append(k)
+    if strict and (missing or unexpected):
+        raise RuntimeError(f"state_dict mismatch: missing={missing} unexpected={unexpected}")
+    if store is not None:
+        store.refresh_shadow()
+    return missing, unexpected
+
+
+def save_resume(path: str, model: nn.Module, optimizer, epoch: int, step: int,
+                extra: Optional[dict] = None) -> None:
+    torch.save({
+        "model": reference_state_dict(model),
+        "optimizer": optimizer.state_dict() if optimizer is not None else None,
+        "epoch": int(epoch),
+        "step": int(step),
+        "torch_rng": torch.get_rng_state(),
+        "extra": extra or {},
+    }, path)
+
+
+def load_resume(path, model: nn.Module, optimizer=None, store=None) -> dict:
+    blob = torch.load(path, map_location="cpu", weights_only=True)
+    own = model.state_dict(keep_vars=True)
+    with torch.no_grad():
+        for k, v in strip_prefix(blob["model"]).items():
+            if k in own:
+                own[k].data.copy_(v.to(own[k].device, own[k].dtype).reshape(own[k].shape))
+    if store is not None:
+        store.refresh_shadow()
+    if optimizer is not None and blob.get("optimizer") is not None:
+        optimizer.load_state_dict(blob["optimizer"])
+    return blob

@@ -1,0 +1,53 @@
+"""Small shared helpers: config access with defaults, seeding, JSONL metrics."""
+from __future__ import annotations
+
+import json
+import os
+import random
+import time
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+
+def cfg_get(cfg, dotted: str, default: Any = None) -> Any:
+    cur = cfg
+    for part in dotted.split("."):
+        if isinstance(cur, dict) and part in cur:
+            cur = cur[part]
+        else:
+            return default
+    return default if cur is None and default is not None else cur
+
+
+def seed_everything(seed: int, deterministic: bool = False) -> None:
+    """Reference seeding (main.py:146-151): numpy + torch + all GPUs, same seed on every rank."""
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+    if deterministic:
+        torch.use_deterministic_algorithms(True, warn_only=True)
+
+
+class MetricsWriter:
+    """Append-only JSONL metrics stream (epoch, step, loss, lr, images/sec, ...)."""
+
+    def __init__(self, path: Optional[str]):
+        self.f = open(path, "a") if path else None
+
+    def write(self, **kw) -> None:
+        if self.f is None:
+            return
+        kw.setdefault("time", time.time())
+        self.f.write(json.dumps(kw) + "\n")
+        self.f.flush()
+
+    def close(self) -> None:
+        if self.f is not None:
+            self.f.close()
+            self.f = None

@@ -1,0 +1,242 @@
+"""Numerics of every hand-written HIP kernel against a plain PyTorch fp32 reference of the same op
+(run on an MI355X: ``pytest -m gpu``).  Inputs are bf16-representable so the comparison isolates
+the kernel's accumulation error."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from simclr_amd.ops import _ext
+    _ext.require()
+    return torch.ops.simclr_amd
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return (a.float() - b.float()).abs().max().item() / (b.float().abs().max().item() + 1e-6)
+
+
+CONV_CASES = [
+    # N, C, H, W, Co, k, s, p
+    (4, 64, 8, 8, 64, 3, 1, 1),
+    (3, 64, 9, 9, 128, 3, 2, 1),
+    (2, 128, 8, 8, 256, 1, 1, 0),
+    (2, 256, 8, 8, 512, 1, 2, 0),
+    (5, 8, 8, 8, 64, 3, 1, 3),
+    (2, 8, 16, 16, 64, 7, 2, 3),
+    (1, 64, 5, 5, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(ops, case):
+    from simclr_amd.ops.conv_hip import ConvHipFn
+    N, C, H, W, Co, k, s, p = case
+    torch.manual_seed(0)
+    x = _bf(torch.randn(N, C, H, W, device=DEV)).contiguous(memory_format=torch.channels_last)
+    w = _bf(torch.randn(Co, C, k, k, device=DEV) / math.sqrt(C * k * k)).float()
+    x.requires_grad_(True)
+    wp = w.clone().requires_grad_(True)
+    y = ConvHipFn.apply(x, wp, s, p, False)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, s, p)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    gy = _bf(torch.randn_like(yr))
+    y.backward(gy.contiguous(memory_format=torch.channels_last))
+    yr.backward(gy.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(wp.grad, wr.grad) < 1e-2
+
+
+def test_conv_stats_epilogue(ops):
+    from simclr_amd.ops.conv_hip import ConvHipFn
+    torch.manual_seed(1)
+    x = _bf(torch.randn(8, 64, 16, 16, device=DEV)).contiguous(memory_format=torch.channels_last)
+    w = _bf(torch.randn(64, 64, 3, 3, device=DEV) / 24).float()
+    y = ConvHipFn.apply(x, w, 1, 1, True)
+    stats, nblk = y._simclr_stats
+    st = stats.view(nblk, 2, 64)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64)
+    assert torch.allclose(st[:, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("C,relu,res,S,spatial", [(64, True, False, 2, 8), (256, True, True, 2, 4),
+                                                  (128, False, False, 1, 3), (2048, True, False, 2, 1)])
+def test_batchnorm_train(ops, C, relu, res, S, spatial):
+    from simclr_amd.ops.batchnorm import BatchNorm2d, reference_batch_norm_train
+    from simclr_amd.ops.batchnorm_hip import batch_norm_train
+    from simclr_amd.parallel import state as pstate
+    torch.manual_seed(2)
+    N = 8
+    bn = BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C) + 0.5)
+        bn.bias.copy_(torch.randn(C) * 0.1)
+    bn_ref = BatchNorm2d(C).to(DEV)
+    bn_ref.load_state_dict(bn.state_dict())
+    x = _bf(torch.randn(N, C, spatial, spatial, device=DEV) * 2 + 0.5).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    r = (_bf(torch.randn(N, C, spatial, spatial, device=DEV)).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True) if res else None)
+    y = batch_norm_train(x, bn, S, r, relu, pstate.get())
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if res else None
+    yr = reference_batch_norm_train(xr, bn_ref, S, rr, relu)
+    assert _rel(y, yr) < 2e-2
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(bn.running_var, bn_ref.running_var, atol=1e-3, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == S
+    gy = _bf(torch.randn_like(yr))
+    y.backward(gy.contiguous(memory_format=torch.channels_last))
+    yr.backward(gy.float())
+    assert _rel(x.grad, xr.grad) < 3e-2
+    assert _rel(bn.weight.grad, bn_ref.weight.grad) < 2e-2
+    assert _rel(bn.bias.grad, bn_ref.bias.grad) < 2e-2
+    if res:
+        assert _rel(r.grad, rr.grad) < 2e-2
+
+
+def test_avgpool(ops):
+    from simclr_amd.ops.pooling_hip import AvgPoolHipFn
+    x = _bf(torch.randn(6, 64, 4, 4, device=DEV)).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    y = AvgPoolHipFn.apply(x)
+    xr = x.detach().float().requires_grad_(True)
+    yr = xr.mean(dim=(2, 3))
+    assert _rel(y, yr) < 1e-2
+    g = _bf(torch.randn(6, 64, device=DEV))
+    y.backward(g)
+    yr.backward(g.float())
+    assert _rel(x.grad, xr.grad) < 1e-2
+
+
+def test_linear(ops):
+    from simclr_amd.ops.gemm_hip import LinearHipFn
+    torch.manual_seed(3)
+    x = _bf(torch.randn(256, 512, device=DEV)).requires_grad_(True)
+    w = _bf(torch.randn(128, 512, device=DEV) / 22).float().requires_grad_(True)
+    b = torch.randn(128, device=DEV).requires_grad_(True)
+    y = LinearHipFn.apply(x, w, b, False)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = F.linear(xr, wr, br)
+    assert _rel(y, yr) < 1e-2
+    g = _bf(torch.randn(256, 128, device=DEV))
+    y.backward(g)
+    yr.backward(g.float())
+    assert _rel(x.grad, xr.grad) < 1e-2
+    assert _rel(w.grad, wr.grad) < 1e-2
+    assert _rel(b.grad, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("n,d,tau", [(64, 128, 0.5), (512, 128, 0.5), (32, 64, 0.1)])
+def test_ntxent(ops, n, d, tau):
+    from simclr_amd.loss.ntxent import NTXent, nt_xent_torch
+    torch.manual_seed(4)
+    z = _bf(torch.randn(2 * n, d, device=DEV)).requires_grad_(True)
+    loss = NTXent(tau)(z)
+    zr = z.detach().float().requires_grad_(True)
+    lr = nt_xent_torch(zr, n, tau)
+    assert abs(loss.item() - lr.item()) < 1e-4 * max(1.0, abs(lr.item()))
+    loss.backward()
+    lr.backward()
+    assert _rel(z.grad, zr.grad) < 1e-2
+
+
+def test_ntxent_matches_reference_formulation(ops):
+    """HIP NT-Xent == the reference's mask/concat formulation (loss.py:33-65)."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from bench.torch_reference import nt_xent_reference
+    from simclr_amd.loss.ntxent import NTXent
+    torch.manual_seed(5)
+    v0 = _bf(torch.randn(128, 128, device=DEV))
+    v1 = _bf(torch.randn(128, 128, device=DEV))
+    a = NTXent(0.5)(v0, v1).item()
+    b = nt_xent_reference(v0.float(), v1.float(), 0.5).item()
+    assert abs(a - b) < 1e-4
+
+
+def test_lars_kernel_matches_torch(ops):
+    from simclr_amd.models import ContrastiveModel
+    from simclr_amd.optim.lars import FusedLARS, weight_decay_per_param
+    from simclr_amd.parallel.flat import FlatParamStore
+    from simclr_amd.ops import registry
+    torch.manual_seed(6)
+    stores = []
+    for _ in range(2):
+        torch.manual_seed(6)
+        m = ContrastiveModel("resnet18").to(DEV)
+        st = FlatParamStore(m, DEV, shadow_dtype=torch.bfloat16)
+        stores.append(st)
+    g = torch.randn(stores[0].total, device=DEV) * 1e-2
+    for st in stores:
+        st.grad.copy_(g)
+    opts = [FusedLARS(st, weight_decay_per_param(st, 1e-4), lr0=2.0, warmup_steps=3,
+                      total_steps=20) for st in stores]
+    for _ in range(5):
+        opts[0].step()
+        registry.set_backend("torch")
+        try:
+            opts[1].step()
+        finally:
+            registry.set_backend("auto")
+    assert torch.allclose(stores[0].master, stores[1].master, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(opts[0].mom, opts[1].mom, rtol=1e-4, atol=1e-6)
+    assert torch.equal(stores[0].shadow, stores[0].master.to(torch.bfloat16))
+    assert abs(opts[0].lr_t.item() - opts[1].lr_t.item()) < 1e-6
+
+
+def test_augment_matches_numpy(ops):
+    from simclr_amd.data import augment_ref
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, size=(16, 32, 32, 3), dtype=np.uint8)
+    idx = np.arange(16, dtype=np.int64)
+    n, views = 16, 2
+    out = torch.empty((views * n, 32, 32, 8), device=DEV, dtype=torch.bfloat16)
+    params = torch.empty((views * n * 16,), device=DEV, dtype=torch.float32)
+    ops.augment(torch.from_numpy(imgs).to(DEV), torch.from_numpy(idx).to(DEV), n, views, 32, 32, 8,
+                0.5, 7, 3, 0, 1, out, params)
+    ref = augment_ref.augment_batch(imgs, idx, views, 32, 32, 0.5, 7, 3)
+    got = out.float().cpu().numpy()[..., :3].transpose(0, 3, 1, 2)
+    assert (out.float()[..., 3:] == 0).all()
+    diff = np.abs(got - ref)
+    # bf16 output quantisation + float transcendental differences: almost all pixels equal
+    assert np.mean(diff < 2.5 / 255 + 4e-3) > 0.97
+    # and the sampled parameters agree for (nearly) every image
+    P = params.view(views * n, 16).cpu().numpy()
+    same = 0
+    for v in range(views):
+        for b in range(n):
+            p = augment_ref.sample_params(
+                augment_ref.Rng(augment_ref.image_key(7, 3, v, b)), 32, 32, 0.5)
+            row = P[v * n + b]
+            same += int(row[0] == p["ci"] and row[1] == p["cj"] and row[2] == p["ch"]
+                        and row[3] == p["cw"] and bool(row[4]) == p["flip"])
+    assert same >= views * n - 1
+
+
+def test_augment_plain_mode(ops):
+    rng = np.random.default_rng(1)
+    imgs = torch.from_numpy(rng.integers(0, 256, size=(4, 32, 32, 3), dtype=np.uint8)).to(DEV)
+    out = torch.empty((4, 32, 32, 8), device=DEV, dtype=torch.bfloat16)
+    ops.augment(imgs, None, 4, 1, 32, 32, 8, 0.5, 0, 0, 0, 0, out, None)
+    ref = imgs.float() / 255
+    assert torch.allclose(out.float()[..., :3], ref, atol=4e-3)
