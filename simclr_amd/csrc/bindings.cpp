@@ -3,6 +3,7 @@
 // shapes / dtypes / devices the kernels assume before any launch (a bad shape must never reach a
 // hand-written kernel: an out-of-bounds access can take the whole node down).
 #include <ATen/core/Tensor.h>
+#include <ATen/ops/empty.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/util/Exception.h>
 #include <torch/library.h>
@@ -146,7 +147,14 @@ void bn_stats(const Tensor& x, int64_t S, const Tensor& partial) {
 
 void bn_reduce(const Tensor& partial, int64_t nblk, int64_t S, int64_t C, const Tensor& stats) {
   TORCH_CHECK(partial.numel() >= S * nblk * 2 * C && stats.numel() >= 2 * S * C, "bn_reduce sizes");
-  bn_reduce_partials(f32(partial, "partial"), nblk, S, C, f32w(stats, "stats"), cur_stream());
+  const int G = bn_reduce_groups((int)nblk);
+  at::Tensor ws;
+  float* wsp = nullptr;
+  if (G > 1) {
+    ws = at::empty({S * G * 2 * C}, stats.options());
+    wsp = ws.data_ptr<float>();
+  }
+  bn_reduce_partials(f32(partial, "partial"), nblk, S, C, f32w(stats, "stats"), wsp, cur_stream());
 }
 
 void bn_final(const Tensor& stats, int64_t S, int64_t C, double count, double eps, double momentum,

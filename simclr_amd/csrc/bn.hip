@@ -31,14 +31,23 @@ __global__ __launch_bounds__(256) void k_bn_stats(const uint16_t* __restrict__ x
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
     if (rlane < RPB) {
-      for (int r = rbeg + rlane; r < rend; r += RPB) {
-        const u32x4 v = *(const u32x4*)(xs + (size_t)r * C + cc * 8);
+      // rows >= rend read as zero through the buffer descriptor: they add nothing
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)xs, (short)0, (int)(uint32_t)((size_t)rend * C * 2), 0x00020000);
+      for (int r0 = rbeg + rlane; r0 < rend; r0 += RPB * 4) {
+        u32x4 v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float a = lo_bf(v[e]), b = hi_bf(v[e]);
-          s1[2 * e] += a; s2[2 * e] += a * a;
-          s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
-        }
+        for (int u = 0; u < 4; ++u)
+          v[u] = __builtin_amdgcn_raw_buffer_load_b128(
+              rx, (uint32_t)(((size_t)(r0 + u * RPB) * C + cc * 8) * 2), 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = lo_bf(v[u][e]), b = hi_bf(v[u][e]);
+            s1[2 * e] += a; s2[2 * e] += a * a;
+            s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
+          }
       }
     }
     // reduce over RPB row lanes through LDS: red[rlane][cchunk][e][2]
@@ -64,6 +73,42 @@ __global__ __launch_bounds__(256) void k_bn_stats(const uint16_t* __restrict__ x
   }
 }
 
+// Level 1: grid (ceil(C/64), S, G); block = 64 channels x 4 row lanes; each block sums a slice of
+// the nblk partial rows of one segment -> level-2 partials [S][G][2][C].  Enough blocks to spread
+// the (latency-bound) read over the chip; order of summation fixed => deterministic.
+__global__ __launch_bounds__(256) void k_reduce_partials_l1(const float* __restrict__ partial,
+                                                            int nblk, int S, int C, int G,
+                                                            float* __restrict__ l2) {
+  __shared__ float red[4][64][2];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane = threadIdx.x >> 6;
+  const int s = blockIdx.y, gz = blockIdx.z;
+  const int per = (nblk + G - 1) / G;
+  const int beg = gz * per;
+  const int end = min(nblk, beg + per);
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    const float* src = partial + (size_t)s * nblk * 2 * C;
+#pragma unroll 4
+    for (int i = beg + lane; i < end; i += 4) {
+      a += src[(size_t)i * 2 * C + c];
+      b += src[(size_t)i * 2 * C + C + c];
+    }
+  }
+  red[lane][threadIdx.x & 63][0] = a;
+  red[lane][threadIdx.x & 63][1] = b;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    const int t = threadIdx.x & 63;
+    a = red[0][t][0] + red[1][t][0] + red[2][t][0] + red[3][t][0];
+    b = red[0][t][1] + red[1][t][1] + red[2][t][1] + red[3][t][1];
+    float* dst = l2 + (((size_t)s * G + gz) * 2) * C;
+    dst[c] = a;
+    dst[C + c] = b;
+  }
+}
+
+// Level 2: stats[2][S][C] = Σ_g l2[s][g][*][c]
 __global__ void k_reduce_partials(const float* __restrict__ partial, int nblk, int S, int C,
                                   float* __restrict__ stats) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over S*C
@@ -71,6 +116,7 @@ __global__ void k_reduce_partials(const float* __restrict__ partial, int nblk, i
   const int s = idx / C, c = idx % C;
   float a = 0.f, b = 0.f;
   const float* src = partial + (size_t)s * nblk * 2 * C;
+#pragma unroll 8
   for (int i = 0; i < nblk; ++i) {
     a += src[(size_t)i * 2 * C + c];
     b += src[(size_t)i * 2 * C + C + c];
@@ -102,6 +148,14 @@ __global__ void k_bn_finalize(const float* __restrict__ stats, int S, int C, flo
   if (running_var) running_var[c] = rv;
 }
 
+// grid (nbx, S): segment-uniform scale/shift in registers, U rows in flight per thread through
+// raw buffer loads (out-of-range rows read as zero, so the loads need no branches).
+constexpr int UNR = 4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(uint32_t)bytes, 0x00020000);
+}
+
 __global__ __launch_bounds__(256) void k_bn_apply(const uint16_t* __restrict__ x,
                                                   const uint16_t* __restrict__ res,
                                                   uint16_t* __restrict__ y,
@@ -113,50 +167,59 @@ __global__ __launch_bounds__(256) void k_bn_apply(const uint16_t* __restrict__ x
   const int TPR = CH < 256 ? CH : 256;
   const int RPB = 256 / TPR;
   const int Rs = R / S;
+  const int seg = blockIdx.y;
   const int cc0 = threadIdx.x % TPR;
   const int rl = threadIdx.x / TPR;
   if (rl >= RPB) return;
+  const size_t sbase = (size_t)seg * Rs * C;
+  const size_t sbytes = (size_t)Rs * C * 2;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x + sbase, sbytes);
+  const __amdgpu_buffer_rsrc_t rr = rsrc(res ? res + sbase : x + sbase, sbytes);
   for (int cc = cc0; cc < CH; cc += TPR) {
     float sc[8], sh[8];
-    int seg_cached = -1;
-    for (int r = blockIdx.x * RPB + rl; r < R; r += gridDim.x * RPB) {
-      const int seg = r / Rs;
-      if (seg != seg_cached) {
-        seg_cached = seg;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = cc * 8 + e;
-          const float mean = mi[seg * C + c], inv = mi[S * C + seg * C + c];
-          const float g = gamma ? gamma[c] : 1.f;
-          const float b = beta ? beta[c] : 0.f;
-          sc[e] = g * inv;
-          sh[e] = b - mean * g * inv;
-        }
-      }
-      const size_t off = (size_t)r * C + cc * 8;
-      const u32x4 v = *(const u32x4*)(x + off);
-      float o[8];
+    for (int e = 0; e < 8; ++e) {
+      const int c = cc * 8 + e;
+      const float mean = mi[seg * C + c], inv = mi[S * C + seg * C + c];
+      const float g = gamma ? gamma[c] : 1.f;
+      const float b = beta ? beta[c] : 0.f;
+      sc[e] = g * inv;
+      sh[e] = b - mean * g * inv;
+    }
+    for (int r0 = blockIdx.x * RPB * UNR + rl; r0 < Rs; r0 += gridDim.x * RPB * UNR) {
+      u32x4 v[UNR], rv[UNR];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[2 * e] = lo_bf(v[e]) * sc[2 * e] + sh[2 * e];
-        o[2 * e + 1] = hi_bf(v[e]) * sc[2 * e + 1] + sh[2 * e + 1];
+      for (int u = 0; u < UNR; ++u) {
+        const uint32_t off = (uint32_t)(((size_t)(r0 + u * RPB) * C + cc * 8) * 2);
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+        if (res) rv[u] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
       }
-      if (res) {
-        const u32x4 rv = *(const u32x4*)(res + off);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * RPB;
+        if (r >= Rs) break;
+        float o[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          o[2 * e] += lo_bf(rv[e]);
-          o[2 * e + 1] += hi_bf(rv[e]);
+          o[2 * e] = lo_bf(v[u][e]) * sc[2 * e] + sh[2 * e];
+          o[2 * e + 1] = hi_bf(v[u][e]) * sc[2 * e + 1] + sh[2 * e + 1];
         }
-      }
-      if (relu) {
+        if (res) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], 0.f);
-      }
-      u32x4 w;
+          for (int e = 0; e < 4; ++e) {
+            o[2 * e] += lo_bf(rv[u][e]);
+            o[2 * e + 1] += hi_bf(rv[u][e]);
+          }
+        }
+        if (relu) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) w[e] = pack2bf(o[2 * e], o[2 * e + 1]);
-      *(u32x4*)(y + off) = w;
+          for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], 0.f);
+        }
+        u32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = pack2bf(o[2 * e], o[2 * e + 1]);
+        *(u32x4*)(y + sbase + (size_t)r * C + cc * 8) = w;
+      }
     }
   }
 }
@@ -223,27 +286,40 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint16_t* __restric
       inv[e] = mi[S * C + seg * C + cc * 8 + e];
     }
     if (rlane < RPB) {
-      for (int r = rbeg + rlane; r < rend; r += RPB) {
-        const size_t off = base + (size_t)r * C + cc * 8;
-        const u32x4 vd = *(const u32x4*)(dy + off);
-        const u32x4 vx = *(const u32x4*)(x + off);
-        u32x4 vy = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-        if (relu) vy = *(const u32x4*)(y + off);
+      // rows >= rend read as zero (dy = 0 contributes nothing)
+      const uint32_t nb = (uint32_t)((size_t)rend * C * 2);
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dy + base),
+                                                                          (short)0, (int)nb, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base),
+                                                                          (short)0, (int)nb, 0x00020000);
+      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((relu ? y : x) + base), (short)0, (int)nb, 0x00020000);
+      for (int r0 = rbeg + rlane; r0 < rend; r0 += RPB * 4) {
+        u32x4 vd[4], vx[4], vy[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int k = 2 * e + h;
-            float g = h ? hi_bf(vd[e]) : lo_bf(vd[e]);
-            if (relu) {
-              const float yy = h ? hi_bf(vy[e]) : lo_bf(vy[e]);
-              g = yy > 0.f ? g : 0.f;
-            }
-            const float xh = ((h ? hi_bf(vx[e]) : lo_bf(vx[e])) - mean[k]) * inv[k];
-            s1[k] += g;
-            s2[k] += g * xh;
-          }
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t off = (uint32_t)(((size_t)(r0 + u * RPB) * C + cc * 8) * 2);
+          vd[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0);
+          vx[u] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+          if (relu) vy[u] = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int k = 2 * e + h;
+              float g = h ? hi_bf(vd[u][e]) : lo_bf(vd[u][e]);
+              if (relu) {
+                const float yy = h ? hi_bf(vy[u][e]) : lo_bf(vy[u][e]);
+                g = yy > 0.f ? g : 0.f;
+              }
+              const float xh = ((h ? hi_bf(vx[u][e]) : lo_bf(vx[u][e])) - mean[k]) * inv[k];
+              s1[k] += g;
+              s2[k] += g * xh;
+            }
+          }
       }
     }
     __syncthreads();
@@ -302,62 +378,74 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const uint16_t* __restrict
   const int TPR = CH < 256 ? CH : 256;
   const int RPB = 256 / TPR;
   const int Rs = R / S;
+  const int seg = blockIdx.y;
   const int cc0 = threadIdx.x % TPR;
   const int rl = threadIdx.x / TPR;
   if (rl >= RPB) return;
+  const size_t sbase = (size_t)seg * Rs * C;
+  const size_t sbytes = (size_t)Rs * C * 2;
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dy + sbase, sbytes);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x + sbase, sbytes);
+  const __amdgpu_buffer_rsrc_t ry = rsrc(relu ? y + sbase : x + sbase, sbytes);
   for (int cc = cc0; cc < CH; cc += TPR) {
     float A[8], B[8], D[8];
-    int seg_cached = -1;
-    for (int r = blockIdx.x * RPB + rl; r < R; r += gridDim.x * RPB) {
-      const int seg = r / Rs;
-      if (seg != seg_cached) {
-        seg_cached = seg;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = cc * 8 + e;
-          A[e] = coef[seg * C + c];
-          B[e] = coef[S * C + seg * C + c];
-          D[e] = coef[2 * S * C + seg * C + c];
-        }
+    for (int e = 0; e < 8; ++e) {
+      const int c = cc * 8 + e;
+      A[e] = coef[seg * C + c];
+      B[e] = coef[S * C + seg * C + c];
+      D[e] = coef[2 * S * C + seg * C + c];
+    }
+    for (int r0 = blockIdx.x * RPB * UNR + rl; r0 < Rs; r0 += gridDim.x * RPB * UNR) {
+      u32x4 vd[UNR], vx[UNR], vy[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const uint32_t off = (uint32_t)(((size_t)(r0 + u * RPB) * C + cc * 8) * 2);
+        vd[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0);
+        vx[u] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+        if (relu) vy[u] = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
       }
-      const size_t off = (size_t)r * C + cc * 8;
-      const u32x4 vd = *(const u32x4*)(dy + off);
-      const u32x4 vx = *(const u32x4*)(x + off);
-      u32x4 vy = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-      if (relu) vy = *(const u32x4*)(y + off);
-      u32x4 wdx, wg;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float o[2], gg[2];
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * RPB;
+        if (r >= Rs) break;
+        u32x4 wdx, wg;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int k = 2 * e + h;
-          float g = h ? hi_bf(vd[e]) : lo_bf(vd[e]);
-          if (relu) {
-            const float yy = h ? hi_bf(vy[e]) : lo_bf(vy[e]);
-            g = yy > 0.f ? g : 0.f;
+        for (int e = 0; e < 4; ++e) {
+          float o[2], gg[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = 2 * e + h;
+            float g = h ? hi_bf(vd[u][e]) : lo_bf(vd[u][e]);
+            if (relu) {
+              const float yy = h ? hi_bf(vy[u][e]) : lo_bf(vy[u][e]);
+              g = yy > 0.f ? g : 0.f;
+            }
+            const float xv = h ? hi_bf(vx[u][e]) : lo_bf(vx[u][e]);
+            o[h] = A[k] * g + B[k] * xv + D[k];
+            gg[h] = g;
           }
-          const float xv = h ? hi_bf(vx[e]) : lo_bf(vx[e]);
-          o[h] = A[k] * g + B[k] * xv + D[k];
-          gg[h] = g;
+          wdx[e] = pack2bf(o[0], o[1]);
+          wg[e] = pack2bf(gg[0], gg[1]);
         }
-        wdx[e] = pack2bf(o[0], o[1]);
-        wg[e] = pack2bf(gg[0], gg[1]);
+        const size_t off = sbase + (size_t)r * C + cc * 8;
+        *(u32x4*)(dx + off) = wdx;
+        if (dres) *(u32x4*)(dres + off) = wg;
       }
-      *(u32x4*)(dx + off) = wdx;
-      if (dres) *(u32x4*)(dres + off) = wg;
     }
   }
 }
 
-int apply_grid(int R, int C) {
+int apply_grid(int R, int C, int S) {
   const int CH = C / 8;
   const int TPR = CH < 256 ? CH : 256;
   const int RPB = 256 / TPR;
-  int blocks = (R + RPB - 1) / RPB;
-  // each thread should handle several rows for amortised scale/shift loads
-  blocks = (blocks + 7) / 8;
-  if (blocks > 4096) blocks = 4096;
+  const int Rs = R / S;
+  int blocks = (Rs + RPB * UNR - 1) / (RPB * UNR);
+  // ~2 iterations of UNR rows per thread; cap the grid at ~8 blocks per CU per segment
+  blocks = (blocks + 1) / 2;
+  const int cap = 2048 / S;
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   return blocks;
 }
@@ -385,8 +473,23 @@ void bn_stats_partial(const uint16_t* x, int R, int C, int S, float* partial, in
   HIP_CHECK_LAUNCH();
 }
 
-void bn_reduce_partials(const float* partial, int nblk, int S, int C, float* stats, hipStream_t s) {
+int bn_reduce_groups(int nblk) {
+  if (nblk <= 32) return 1;
+  int g = (nblk + 31) / 32;  // ~32 rows per level-1 block
+  return g > 64 ? 64 : g;
+}
+
+void bn_reduce_partials(const float* partial, int nblk, int S, int C, float* stats, float* ws,
+                        hipStream_t s) {
   const int n = S * C;
+  const int G = bn_reduce_groups(nblk);
+  if (G > 1) {
+    hipLaunchKernelGGL(k_reduce_partials_l1, dim3((C + 63) / 64, S, G), dim3(256), 0, s, partial,
+                       nblk, S, C, G, ws);
+    HIP_CHECK_LAUNCH();
+    partial = ws;
+    nblk = G;
+  }
   hipLaunchKernelGGL(k_reduce_partials, dim3((n + 255) / 256), dim3(256), 0, s, partial, nblk, S, C,
                      stats);
   HIP_CHECK_LAUNCH();
@@ -403,7 +506,7 @@ void bn_finalize(const float* stats, int S, int C, float count, float eps, float
 void bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* mi,
               const float* gamma, const float* beta, int R, int C, int S, int relu,
               hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_apply, dim3(apply_grid(R, C)), dim3(256), 0, s, x, res, y, mi, gamma,
+  hipLaunchKernelGGL(k_bn_apply, dim3(apply_grid(R, C, S), S), dim3(256), 0, s, x, res, y, mi, gamma,
                      beta, R, C, S, relu);
   HIP_CHECK_LAUNCH();
 }
@@ -436,7 +539,7 @@ void bn_bwd_finalize(const float* sums, const float* mi, const float* gamma, int
 
 void bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef,
                   int R, int C, int S, int relu, uint16_t* dx, uint16_t* dres, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(apply_grid(R, C)), dim3(256), 0, s, dy, y, x, coef, R, C,
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(apply_grid(R, C, S), S), dim3(256), 0, s, dy, y, x, coef, R, C,
                      S, relu, dx, dres);
   HIP_CHECK_LAUNCH();
 }

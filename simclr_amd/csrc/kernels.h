@@ -30,8 +30,9 @@ void conv_weight_transform(const uint16_t* W, uint16_t* Wt, int Co, int KH, int 
 void bn_stats_partial(const uint16_t* x, int R, int C, int S, float* partial, int* nblk_per_seg,
                       hipStream_t s);
 int bn_stats_blocks_per_seg(int R, int C, int S);
+int bn_reduce_groups(int nblk);  // level-1 groups; workspace = S*groups*2*C floats
 void bn_reduce_partials(const float* partial, int nblk_per_seg, int S, int C, float* stats,
-                        hipStream_t s);
+                        float* ws, hipStream_t s);
 void bn_finalize(const float* stats, int S, int C, float count, float eps, float momentum,
                  float* running_mean, float* running_var, float* mean_invstd, int64_t* nbt,
                  hipStream_t s);
