@@ -81,7 +81,7 @@ class Conv2d(nn.Conv2d):
         if x.dtype == torch.bfloat16 and registry.use_hip(x):
             from . import conv_hip
             out = conv_hip.conv2d(x, None, self.stride, self.padding, weight_param=self.weight,
-                                  emit_stats=self.emit_bn_stats)
+                                  emit_stats=self.emit_bn_stats and self.training)
             if out is not None:
                 return out
         w = effective_weight(self)

@@ -14,7 +14,7 @@ def linear_module(mod, x: torch.Tensor) -> torch.Tensor:
     if x.dtype == torch.bfloat16 and registry.use_hip(x):
         from . import gemm_hip
         out = gemm_hip.linear(x, None, None, weight_param=mod.weight, bias_param=mod.bias,
-                              emit_stats=getattr(mod, "emit_bn_stats", False))
+                              emit_stats=getattr(mod, "emit_bn_stats", False) and mod.training)
         if out is not None:
             return out
     w = effective_weight(mod)
