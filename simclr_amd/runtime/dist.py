@@ -5,9 +5,9 @@ rendezvous, ``rank = cfg.distributed.local_rank`` (wrong across nodes, SURVEY Q1
 ``torch.cuda.set_device(rank)``; ``cleanup()`` is never called.
 
 Here: the *global* rank / world size come from ``RANK`` / ``WORLD_SIZE`` (written by our
-launcher and by torchrun), the GPU from ``LOCAL_RANK``; without those variables the Hydra keys
-``distributed.local_rank`` / ``distributed.world_size`` are honoured when ``MASTER_ADDR`` is set,
-else the run is single-process.  Backend: ``nccl`` (= RCCL over xGMI on ROCm) on GPUs, ``gloo``
+launcher and by torchrun), the GPU from ``LOCAL_RANK``; without those variables the run is single-process (the
+Hydra keys ``distributed.local_rank`` / ``distributed.world_size`` that launch.py still appends
+for command-line compatibility must agree with the environment).  Backend: ``nccl`` (= RCCL over xGMI on ROCm) on GPUs, ``gloo``
 on CPU.  A process-group timeout makes a dead peer an error instead of a hang.
 """
 from __future__ import annotations
@@ -29,11 +29,8 @@ def resolve_world(cfg=None):
         rank = int(env["RANK"])
         local = int(env.get("LOCAL_RANK", rank))
         return rank, world, local
-    if cfg is not None and "distributed" in cfg and "MASTER_ADDR" in env:
-        d = cfg["distributed"]
-        world = int(d.get("world_size", 1))
-        local = int(d.get("local_rank", 0))
-        return local, world, local
+    # Without RANK/WORLD_SIZE (not launched by launch.py / torchrun) run single-process: the
+    # reference's default ``distributed.world_size=4`` would otherwise wait forever for peers.
     return 0, 1, 0
 
 

@@ -1,0 +1,119 @@
+"""Multi-process correctness without a cluster: gloo, world_size 2, CPU.
+
+* flat-store bucketed DDP + segmented SyncBN + global-negative NT-Xent (``loss.gather``) on 2
+  ranks with n images each gives the same parameter gradients as 1 process with 2n images;
+* SyncBN running statistics agree with the single-process batch statistics;
+* the fail-fast launcher terminates surviving ranks when one rank dies.
+"""
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+import textwrap
+import time
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(n_total, size=16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    v0 = torch.rand(n_total, 3, size, size, generator=g)
+    v1 = torch.rand(n_total, 3, size, size, generator=g)
+    return v0, v1
+
+
+def _model(seed=0):
+    from simclr_amd.models import ContrastiveModel
+    torch.manual_seed(seed)
+    return ContrastiveModel("resnet18", d=32)
+
+
+def _worker(rank, world, port, n, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from simclr_amd.loss.ntxent import NTXent
+    from simclr_amd.parallel import state as pstate
+    from simclr_amd.parallel.flat import FlatParamStore
+    pstate.set_state(rank=rank, world_size=world, local_rank=rank, group=dist.group.WORLD)
+    torch.set_num_threads(1)
+    m = _model()
+    store = FlatParamStore(m, "cpu", shadow_dtype=None, bucket_mb=1.0, first_bucket_mb=0.25)
+    store.broadcast_from(0)
+    v0, v1 = _data(n * world)
+    x = torch.cat([v0[rank * n:(rank + 1) * n], v1[rank * n:(rank + 1) * n]])
+    z = m(x, segments=2)
+    loss = NTXent(0.5, gather=True)(z)
+    store.zero_grad()
+    loss.backward()
+    store.finish()
+    if rank == 0:
+        torch.save({"grad": store.grad.clone() / world, "names": store.names,
+                    "rm": m.f.layer1[0].bn1.running_mean.clone(), "loss": loss.detach()},
+                   os.path.join(out_dir, "r0.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_syncbn_gather_equivalence(tmp_path):
+    from simclr_amd.loss.ntxent import NTXent
+    from simclr_amd.parallel import state as pstate
+    from simclr_amd.parallel.flat import FlatParamStore
+    n, world = 4, 2
+    mp.spawn(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True)
+    got = torch.load(tmp_path / "r0.pt", weights_only=True)
+    pstate.reset()
+    m = _model()
+    store = FlatParamStore(m, "cpu", shadow_dtype=None)
+    v0, v1 = _data(n * world)
+    z = m(torch.cat([v0, v1]), segments=2)
+    loss = NTXent(0.5)(z)
+    store.zero_grad()
+    loss.backward()
+    assert got["names"] == store.names
+    rel = (got["grad"] - store.grad).abs().max() / store.grad.abs().max()
+    assert rel < 1e-4, float(rel)
+    assert torch.allclose(got["rm"], m.f.layer1[0].bn1.running_mean, atol=1e-5)
+
+
+def test_launcher_fail_fast(tmp_path):
+    script = tmp_path / "job.py"
+    script.write_text(textwrap.dedent("""
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(120)
+    """))
+    t0 = time.time()
+    r = subprocess.run([sys.executable, str(ROOT / "launch.py"), "--nproc_per_node=2", "--use_env",
+                        "--kill_grace=2", str(script)], cwd=str(tmp_path), timeout=90)
+    assert r.returncode == 3
+    assert time.time() - t0 < 60
+
+
+def test_launcher_env_and_overrides():
+    from simclr_amd.runtime.launcher import build_commands, parse_args
+    cmds = build_commands(parse_args(["--nproc_per_node=2", "--nnodes=2", "--node_rank=1", "-m",
+                                      "main", "parameter.epochs=1"]))
+    (c0, e0), (c1, e1) = cmds
+    assert e0["RANK"] == "2" and e1["RANK"] == "3" and e1["LOCAL_RANK"] == "1"
+    assert e0["WORLD_SIZE"] == "4"
+    assert c1[-3:] == ["distributed.local_rank=1", "distributed.world_size=4",
+                       "parameter.epochs=1"]
+    assert c0[1:4] == ["-u", "-m", "main"]
