@@ -68,8 +68,36 @@ ConvGeom geom_from(const std::vector<int64_t>& v) {
 }
 
 // ------------------------------------------------------------------------------- conv
+ConvFusion fusion_from(const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
+                       int64_t pro_seg_rows, bool pro_relu, int64_t pro_S, int64_t epi_mode,
+                       const c10::optional<Tensor>& epi_a, const c10::optional<Tensor>& epi_b,
+                       int64_t C, int64_t out_numel) {
+  ConvFusion f;
+  f.pro_sc = optf32(pro_sc, "pro_sc");
+  f.pro_sh = optf32(pro_sh, "pro_sh");
+  TORCH_CHECK((f.pro_sc == nullptr) == (f.pro_sh == nullptr), "prologue needs scale and shift");
+  if (f.pro_sc) {
+    TORCH_CHECK(pro_sc->numel() >= pro_S * C && pro_sh->numel() >= pro_S * C,
+                "prologue scale/shift must be [S][C]");
+  }
+  f.pro_seg_rows = (int)pro_seg_rows;
+  f.pro_relu = pro_relu ? 1 : 0;
+  f.pro_S = (int)pro_S;
+  f.epi_mode = (int)epi_mode;
+  f.epi_a = optbf(epi_a, "epi_a");
+  f.epi_b = optbf(epi_b, "epi_b");
+  TORCH_CHECK(epi_mode >= 0 && epi_mode <= 2, "epi_mode");
+  if (epi_mode >= 1) TORCH_CHECK(f.epi_a && epi_a->numel() >= out_numel, "epilogue operand a");
+  if (epi_mode == 2) TORCH_CHECK(f.epi_b && epi_b->numel() >= out_numel, "epilogue operand b");
+  return f;
+}
+
 void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optional<Tensor>& bias,
-           const c10::optional<Tensor>& stats, std::vector<int64_t> gv) {
+           const c10::optional<Tensor>& stats, std::vector<int64_t> gv,
+           const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
+           int64_t pro_seg_rows, bool pro_relu, int64_t epi_mode,
+           const c10::optional<Tensor>& epi_a, const c10::optional<Tensor>& epi_b,
+           int64_t variant) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -78,22 +106,37 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   TORCH_CHECK(g.ldo % 8 == 0 && g.N % 8 == 0, "igemm: N/ldo must be multiples of 8");
   TORCH_CHECK(out.numel() >= (int64_t)g.Nb * g.OHp * g.OWp * g.ldo, "igemm: out too small");
   TORCH_CHECK(out.numel() * 2 < ((int64_t)1 << 31) * 2, "igemm: out too large");
+  if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
+  const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
+  const int bm = igemm_variant_bm((int)variant);
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
-  if (stats.has_value() && stats->defined()) {
-    const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
-    const int bm = igemm_block_m(g.N);
+  if (stats.has_value() && stats->defined())
     TORCH_CHECK(stats->numel() >= ((M + bm - 1) / bm) * 2 * g.N, "igemm: stats buffer too small");
+  ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, 2, epi_mode, epi_a, epi_b,
+                             g.C, out.numel());
+  if (f.pro_sc) {
+    TORCH_CHECK(pro_seg_rows > 0 && pro_seg_rows % bm == 0 && M % pro_seg_rows == 0,
+                "igemm prologue: segment rows must be a multiple of the tile rows");
+    TORCH_CHECK(pro_sc->numel() >= (M / pro_seg_rows) * g.C, "igemm prologue: [S][C] size");
   }
   conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
-                optf32w(stats, "stats"), cur_stream());
+                optf32w(stats, "stats"), f, (int)variant, cur_stream());
 }
 
 int64_t igemm_bm(int64_t N) { return igemm_block_m((int)N); }
+int64_t igemm_nvariants() { return igemm_num_variants(); }
+int64_t igemm_vbm(int64_t v) { return igemm_variant_bm((int)v); }
+int64_t igemm_vbn(int64_t v) { return igemm_variant_bn((int)v); }
+int64_t wgrad_nvariants() { return wgrad_num_variants(); }
 
-int64_t wgrad_nsplit(std::vector<int64_t> gv) { return wgrad_splits(geom_from(gv)); }
+int64_t wgrad_nsplit(std::vector<int64_t> gv, int64_t variant) {
+  return wgrad_splits(geom_from(gv), (int)variant);
+}
 
 void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tensor& out,
-           std::vector<int64_t> gv, int64_t splits, int64_t creal, double beta) {
+           std::vector<int64_t> gv, int64_t splits, int64_t creal, double beta,
+           const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
+           int64_t pro_seg_rows, bool pro_relu, int64_t pro_S, int64_t variant) {
   const ConvGeom g = geom_from(gv);
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int64_t K = (int64_t)g.KH * g.KW * g.C;
@@ -102,8 +145,15 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
   TORCH_CHECK(partial.numel() >= splits * g.N * K, "wgrad: partial too small");
   TORCH_CHECK(out.numel() == (int64_t)g.N * g.KH * g.KW * creal, "wgrad: out numel mismatch");
   TORCH_CHECK(creal <= g.C && creal > 0, "wgrad: bad creal");
+  TORCH_CHECK(pro_S >= 1 && pro_S <= 2, "wgrad prologue supports at most 2 segments");
+  ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, pro_S, 0, c10::nullopt,
+                             c10::nullopt, g.C, 0);
+  if (f.pro_sc) {
+    // the prologue is indexed by *input* rows, which equal output rows only for 1x1/stride-1
+    TORCH_CHECK(pro_seg_rows > 0 && (int64_t)g.Nb % pro_S == 0, "wgrad prologue geometry");
+  }
   conv_wgrad(g, bf(dY, "dY"), bf(X, "X"), (size_t)X.numel(), f32w(partial, "partial"), (int)splits,
-             f32w(out, "out"), (int)creal, (float)beta, cur_stream());
+             f32w(out, "out"), (int)creal, (float)beta, f, (int)variant, cur_stream());
 }
 
 void weight_transform(const Tensor& W, const Tensor& Wt, std::vector<int64_t> p) {
@@ -367,10 +417,14 @@ void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int6
 }  // namespace
 
 TORCH_LIBRARY(simclr_amd, m) {
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1) -> ()", &igemm);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
-  m.def("wgrad_splits(int[] geom) -> int", &wgrad_nsplit);
-  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta) -> ()", &wgrad);
+  m.def("igemm_nvariants() -> int", &igemm_nvariants);
+  m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);
+  m.def("igemm_variant_bn(int v) -> int", &igemm_vbn);
+  m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
+  m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
+  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);
   m.def("bn_blocks(int R, int C, int S) -> int", &bn_blocks);
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);

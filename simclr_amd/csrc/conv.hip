@@ -14,6 +14,12 @@
 //             is free).  fp32 partial slabs are summed by wgrad_reduce straight into the flat fp32
 //             gradient buffer (OHWI = the im2col K order).
 //
+// Fusions: optional *prologue* applies a per-(segment, channel) affine + ReLU to the gathered A
+// operand on its way into LDS (= the previous BatchNorm's normalise+ReLU, so that BN output is
+// never written to HBM; conv padding stays exactly zero), and the igemm *epilogue* can accumulate
+// a residual (out += r) or a ReLU-masked gradient (out += (y > 0) ? dy : 0) while storing.
+// Several tile shapes are instantiated; the host autotunes one per problem shape.
+//
 // Gather: the A operand is addressed per 16-byte chunk (8 channels) with raw buffer loads whose
 // out-of-range offset returns zeros, so conv padding / M and K tails need no branches around the
 // loads.  Tiles: BM x BN x 64, 256 threads (4 waves), mfma_f32_16x16x32_bf16, LDS double buffer
@@ -37,7 +43,31 @@ struct IgemmArgs {
   int direct_out;
   uint32_t a_bytes, b_bytes;
   int nMb, nNb;
+  // prologue (A operand): a = relu?(x * sc[seg][c] + sh[seg][c]); seg = m / pro_seg_rows
+  const float* pro_sc;
+  const float* pro_sh;
+  int pro_seg_rows, pro_relu;
+  // epilogue: 0 store, 1 out = acc + epi_a, 2 out = acc + (epi_b > 0 ? epi_a : 0)
+  int epi_mode;
+  const uint16_t* epi_a;
+  const uint16_t* epi_b;
 };
+
+__device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const float* sh, bool ok,
+                                              bool relu) {
+  u32x4 w;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float a = lo_bf(v[e]) * sc[2 * e] + sh[2 * e];
+    float b = hi_bf(v[e]) * sc[2 * e + 1] + sh[2 * e + 1];
+    if (relu) {
+      a = fmaxf(a, 0.f);
+      b = fmaxf(b, 0.f);
+    }
+    w[e] = ok ? pack2bf(a, b) : 0u;
+  }
+  return w;
+}
 
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
@@ -88,6 +118,10 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
   }
 
   u32x4 ra[ACH], rb[BCH];
+  bool rok[ACH];
+  float psc[8], psh[8];
+  const bool pro = p.pro_sc != nullptr;
+  const int pseg = pro ? m0 / p.pro_seg_rows : 0;  // block-uniform (host guarantees)
   const uint32_t OOB_A = p.a_bytes, OOB_B = p.b_bytes;
 
   auto gload = [&](int kt) {
@@ -102,8 +136,19 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
       const int ih = a_ih[j] + kh * p.dh;
       const int iw = a_iw[j] + kw * p.dw;
       const bool ok = a_ok[j] && kok && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      rok[j] = ok;
       const uint32_t off = ok ? (uint32_t)((((a_n[j] * p.IH + ih) * p.IW + iw) * p.C + ci) * 2) : OOB_A;
       ra[j] = __builtin_amdgcn_raw_buffer_load_b128(ra_src, off, 0, 0);
+    }
+    if (pro) {
+      const int cc = kok ? ci : 0;
+      const float4* ps = (const float4*)(p.pro_sc + pseg * p.C + cc);
+      const float4* ph = (const float4*)(p.pro_sh + pseg * p.C + cc);
+      const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+      psc[0] = s0.x; psc[1] = s0.y; psc[2] = s0.z; psc[3] = s0.w;
+      psc[4] = s1.x; psc[5] = s1.y; psc[6] = s1.z; psc[7] = s1.w;
+      psh[0] = h0.x; psh[1] = h0.y; psh[2] = h0.z; psh[3] = h0.w;
+      psh[4] = h1.x; psh[5] = h1.y; psh[6] = h1.z; psh[7] = h1.w;
     }
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
@@ -116,7 +161,8 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
     for (int j = 0; j < ACH; ++j) {
       const int row = rbase + 32 * j;
       const int ch = cch ^ (row & 7);
-      *(u32x4*)(As + buf * BM * 64 + row * 64 + ch * 8) = ra[j];
+      const u32x4 v = pro ? affine_relu8(ra[j], psc, psh, rok[j], p.pro_relu != 0) : ra[j];
+      *(u32x4*)(As + buf * BM * 64 + row * 64 + ch * 8) = v;
     }
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
@@ -194,7 +240,7 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
   for (int row = r0; row < BM; row += RSTEP) {
     const int m = m0 + row;
     if (m >= p.M || n >= p.N) continue;
-    const u32x4 v = *(const u32x4*)(Cs + row * CST + ch * 8);
+    u32x4 v = *(const u32x4*)(Cs + row * CST + ch * 8);
     size_t o;
     if (p.direct_out) {
       o = (size_t)m * p.ldo + n;
@@ -204,6 +250,21 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
       const int oh = rem / p.OW;
       const int ow = rem - oh * p.OW;
       o = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
+    }
+    if (p.epi_mode == 1) {
+      const u32x4 r = *(const u32x4*)(p.epi_a + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
+    } else if (p.epi_mode == 2) {
+      const u32x4 d = *(const u32x4*)(p.epi_a + o);
+      const u32x4 y = *(const u32x4*)(p.epi_b + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = lo_bf(y[e]) > 0.f ? lo_bf(d[e]) : 0.f;
+        const float b = hi_bf(y[e]) > 0.f ? hi_bf(d[e]) : 0.f;
+        v[e] = pack2bf(lo_bf(v[e]) + a, hi_bf(v[e]) + b);
+      }
     }
     *(u32x4*)(p.out + o) = v;
     if (p.stats != nullptr) {
@@ -247,6 +308,9 @@ struct WgradArgs {
   int ish, isw, dh, dw, ih0, iw0;
   uint32_t dy_bytes, x_bytes;
   int iters_per_split, splits, nCo, nKk;
+  const float* pro_sc;  // X-operand prologue, [S<=2][C]
+  const float* pro_sh;
+  int pro_seg_rows, pro_relu, pro_S;
 };
 
 template <int BCO, int BKK, int WM, int WN>
@@ -291,6 +355,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
   const int OHW = p.OH * p.OW;
 
   u32x4 rd[DCH], rx[XCH];
+  bool xok[XCH];
+  bool xseg[XCH];
+  const bool pro = p.pro_sc != nullptr;
+  float psc0[8], psh0[8], psc1[8], psh1[8];
+  if (pro) {
+    const int cc = k_ok ? ci : 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      psc0[e] = p.pro_sc[cc + e];
+      psh0[e] = p.pro_sh[cc + e];
+      psc1[e] = p.pro_S > 1 ? p.pro_sc[p.C + cc + e] : psc0[e];
+      psh1[e] = p.pro_S > 1 ? p.pro_sh[p.C + cc + e] : psh0[e];
+    }
+  }
   const int mbeg = split * p.iters_per_split * 64;
   const int mend_raw = mbeg + p.iters_per_split * 64;
   const int mend = mend_raw < p.M ? mend_raw : p.M;
@@ -317,6 +395,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
       const int ih = oh * p.ish + p.ih0 + kh * p.dh;
       const int iw = ow * p.isw + p.iw0 + kw * p.dw;
       ok = ok && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      xok[j] = ok;
+      xseg[j] = pro && m >= p.pro_seg_rows;
       const uint32_t off = ok ? (uint32_t)((((n * p.IH + ih) * p.IW + iw) * p.C + ci) * 2) : p.x_bytes;
       rx[j] = __builtin_amdgcn_raw_buffer_load_b128(rx_src, off, 0, 0);
     }
@@ -326,8 +406,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
     for (int j = 0; j < DCH; ++j)
       *(u32x4*)(Ds + buf * 64 * SD + (drow + RD * j) * SD + dch * 8) = rd[j];
 #pragma unroll
-    for (int j = 0; j < XCH; ++j)
-      *(u32x4*)(Xs + buf * 64 * SX + (xrow + RX * j) * SX + xch * 8) = rx[j];
+    for (int j = 0; j < XCH; ++j) {
+      u32x4 v = rx[j];
+      if (pro)
+        v = xseg[j] ? affine_relu8(v, psc1, psh1, xok[j], p.pro_relu != 0)
+                    : affine_relu8(v, psc0, psh0, xok[j], p.pro_relu != 0);
+      *(u32x4*)(Xs + buf * 64 * SX + (xrow + RX * j) * SX + xch * 8) = v;
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -460,12 +545,32 @@ void launch_igemm(const IgemmArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+template <int BCO, int BKK, int WM, int WN>
+void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
+  WgradArgs a = a0;
+  a.nCo = (a.N + BCO - 1) / BCO;
+  a.nKk = (a.K + BKK - 1) / BKK;
+  const int grid = a.nCo * a.nKk * a.splits;
+  const size_t lds = (size_t)2 * 64 * ((BCO + 8) + (BKK + 8)) * 2;
+  hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN>), dim3(grid), dim3(256), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+// tile variants: {BM, BN}
+constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {64, 64}};
+constexpr int WG_VARIANTS[][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+
 }  // namespace
 
-int igemm_block_m(int N) { return N <= 64 ? 256 : 128; }
+int igemm_num_variants() { return (int)(sizeof(IG_VARIANTS) / sizeof(IG_VARIANTS[0])); }
+int igemm_variant_bm(int v) { return IG_VARIANTS[v][0]; }
+int igemm_variant_bn(int v) { return IG_VARIANTS[v][1]; }
+int igemm_default_variant(int N) { return N <= 64 ? 1 : 0; }
+int igemm_block_m(int N) { return igemm_variant_bm(igemm_default_variant(N)); }
 
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
-                   uint16_t* out, const float* bias, float* stats, hipStream_t s) {
+                   uint16_t* out, const float* bias, float* stats, const ConvFusion& f,
+                   int variant, hipStream_t s) {
   IgemmArgs a{};
   a.A = A; a.B = B; a.out = out; a.bias = bias; a.stats = stats;
   a.M = g.Nb * g.OH * g.OW; a.N = g.N; a.K = g.KH * g.KW * g.C;
@@ -478,19 +583,30 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
                   g.OWp == g.OW) ? 1 : 0;
   a.a_bytes = (uint32_t)(a_elems * 2);
   a.b_bytes = (uint32_t)((size_t)a.N * a.K * 2);
-  if (g.N <= 64) {
-    launch_igemm<256, 64, 4, 1>(a, s);
-  } else {
-    launch_igemm<128, 128, 2, 2>(a, s);
+  a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh; a.pro_seg_rows = f.pro_seg_rows > 0 ? f.pro_seg_rows : a.M;
+  a.pro_relu = f.pro_relu;
+  a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b;
+  if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
+  switch (variant) {
+    case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
+    case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
+    case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
+    case 3: launch_igemm<64, 128, 2, 2>(a, s); break;
+    default: launch_igemm<64, 64, 2, 2>(a, s); break;
   }
 }
 
-int wgrad_splits(const ConvGeom& g) {
+int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
+int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
+
+int wgrad_splits(const ConvGeom& g, int variant) {
+  if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
+  const int bco = WG_VARIANTS[variant][0], bkk = WG_VARIANTS[variant][1];
   const int M = g.Nb * g.OH * g.OW;
   const int K = g.KH * g.KW * g.C;
-  const int tiles = ((g.N + 127) / 128) * ((K + 127) / 128);
+  const int tiles = ((g.N + bco - 1) / bco) * ((K + bkk - 1) / bkk);
   const int iters = (M + 63) / 64;
-  int splits = (1024 + tiles - 1) / tiles;
+  int splits = (768 + tiles - 1) / tiles;
   int max_splits = iters / 8;
   if (max_splits < 1) max_splits = 1;
   if (splits > max_splits) splits = max_splits;
@@ -499,7 +615,8 @@ int wgrad_splits(const ConvGeom& g) {
 }
 
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
-                float* partial, int splits, float* out, int Creal, float beta, hipStream_t s) {
+                float* partial, int splits, float* out, int Creal, float beta,
+                const ConvFusion& f, int variant, hipStream_t s) {
   WgradArgs a{};
   a.dY = dY; a.X = X; a.partial = partial;
   a.M = g.Nb * g.OH * g.OW; a.N = g.N; a.K = g.KH * g.KW * g.C;
@@ -511,18 +628,21 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   const int iters = (a.M + 63) / 64;
   a.splits = splits;
   a.iters_per_split = (iters + splits - 1) / splits;
-  constexpr int BCO = 128, BKK = 128;
-  a.nCo = (a.N + BCO - 1) / BCO;
-  a.nKk = (a.K + BKK - 1) / BKK;
-  const int grid = a.nCo * a.nKk * splits;
-  const size_t lds = (size_t)2 * 64 * ((BCO + 8) + (BKK + 8)) * 2;
-  hipLaunchKernelGGL((wgrad_tn<BCO, BKK, 2, 2>), dim3(grid), dim3(256), lds, s, a);
-  HIP_CHECK_LAUNCH();
+  a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh;
+  a.pro_seg_rows = f.pro_seg_rows > 0 ? f.pro_seg_rows : a.M;
+  a.pro_relu = f.pro_relu; a.pro_S = f.pro_S > 0 ? f.pro_S : 1;
+  if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
+  switch (variant) {
+    case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
+    case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
+    case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;
+    default: launch_wgrad<64, 64, 2, 2>(a, s); break;
+  }
   const int K = a.K;
   if (Creal == g.C) {
     const size_t n4 = (size_t)a.N * K / 4;
     int blocks = (int)((n4 + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
+    if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(wgrad_reduce_vec4, dim3(blocks), dim3(256), 0, s, (const float4*)partial,
                        (float4*)out, splits, n4, beta);
   } else {

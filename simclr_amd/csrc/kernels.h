@@ -17,12 +17,31 @@ struct ConvGeom {
 };
 
 // ---- conv.hip
+// Optional fusions around the implicit GEMM (all pointers nullable / mode 0 = off).
+struct ConvFusion {
+  const float* pro_sc = nullptr;  // A/X-operand prologue: a = relu?(x*sc[seg][c] + sh[seg][c])
+  const float* pro_sh = nullptr;
+  int pro_seg_rows = 0;           // rows per segment (BM must divide it for igemm)
+  int pro_relu = 0;
+  int pro_S = 1;
+  int epi_mode = 0;               // igemm: 1 out = acc + a; 2 out = acc + (b > 0 ? a : 0)
+  const uint16_t* epi_a = nullptr;
+  const uint16_t* epi_b = nullptr;
+};
+int igemm_num_variants();
+int igemm_variant_bm(int v);
+int igemm_variant_bn(int v);
+int igemm_default_variant(int N);
 int igemm_block_m(int N);
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
-                   uint16_t* out, const float* bias, float* stats, hipStream_t s);
-int wgrad_splits(const ConvGeom& g);
+                   uint16_t* out, const float* bias, float* stats, const ConvFusion& f,
+                   int variant, hipStream_t s);
+int wgrad_num_variants();
+int wgrad_default_variant(int N);
+int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
-                float* partial, int splits, float* out, int Creal, float beta, hipStream_t s);
+                float* partial, int splits, float* out, int Creal, float beta,
+                const ConvFusion& f, int variant, hipStream_t s);
 void conv_weight_transform(const uint16_t* W, uint16_t* Wt, int Co, int KH, int KW, int Ci,
                            int KHs, int KWs, int kh0, int sh, int kw0, int sw, hipStream_t s);
 

@@ -21,7 +21,69 @@ from typing import Optional, Tuple
 
 import torch
 
-from . import _ext
+from . import _ext, tuning
+
+
+def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):
+    """Launch the implicit GEMM with the autotuned tile variant for this problem.
+
+    pro = (scale[S][C], shift[S][C], rows_per_segment, relu) applies the previous BatchNorm on the
+    A operand; epi = (mode, a, b) accumulates into the output.  Returns (stats, nblk) or None."""
+    M = geom[0] * geom[4] * geom[5]
+    N = geom[14]
+    psc, psh, seg_rows, prelu = pro if pro is not None else (None, None, 0, False)
+    emode, ea, eb = epi if epi is not None else (0, None, None)
+    cands = []
+    for v in range(ops.igemm_nvariants()):
+        bm = ops.igemm_variant_bm(v)
+        if want_stats and M % bm:
+            continue
+        if psc is not None and seg_rows % bm:
+            continue
+        cands.append(v)
+    default = 1 if N <= 64 else 0
+    if not cands:
+        if psc is not None:
+            raise ValueError("BN prologue fusion impossible for this shape")
+        want_stats = False
+        cands = list(range(ops.igemm_nvariants()))
+    if default not in cands:
+        default = cands[0]
+    key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None)
+
+    def launch(v, o, st):
+        ops.igemm(A, B, o, bias, st, geom, psc, psh, seg_rows, prelu, emode, ea, eb, v)
+
+    def trial(v):
+        bm = ops.igemm_variant_bm(v)
+        st = (torch.empty(((M + bm - 1) // bm) * 2 * N, device=out.device, dtype=torch.float32)
+              if want_stats else None)
+        launch(v, torch.empty_like(out), st)
+
+    v = tuning.pick(key, cands, default, trial)
+    bm = ops.igemm_variant_bm(v)
+    stats = None
+    if want_stats:
+        stats = torch.empty(((M // bm) * 2 * N,), device=out.device, dtype=torch.float32)
+    launch(v, out, stats)
+    return (stats, M // bm) if stats is not None else None
+
+
+def run_wgrad(ops, dY, X, out, geom, creal, pro=None):
+    """Split-M weight gradient (fp32, written to ``out`` = OHWI) with the autotuned variant."""
+    psc, psh, seg_rows, prelu, pS = pro if pro is not None else (None, None, 0, False, 1)
+    N = geom[14]
+    K = geom[6] * geom[7] * geom[3]
+    key = ("wgrad", tuple(geom), creal, psc is not None)
+
+    def launch(v, o):
+        splits = ops.wgrad_splits(geom, v)
+        partial = torch.empty((splits * N * K,), device=dY.device, dtype=torch.float32)
+        ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v)
+
+    v = tuning.pick(key, range(ops.wgrad_nvariants()), 1 if N <= 64 else 0,
+                    lambda vv: launch(vv, torch.empty_like(out)))
+    launch(v, out)
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -74,14 +136,9 @@ class ConvHipFn(torch.autograd.Function):
         w = shadow_ohwi(weight, Cx)
         y = _empty_cl(N, Co, OH, OW, x.device)
         g = fwd_geom(N, H, W, Cx, OH, OW, KH, KW, stride, pad, Co)
-        stats = None
-        M = N * OH * OW
-        bm = ops.igemm_bm(Co)
-        if emit_stats and M % bm == 0:
-            stats = torch.empty(((M // bm) * 2 * Co,), device=x.device, dtype=torch.float32)
-        ops.igemm(xn, w, y.permute(0, 2, 3, 1), None, stats, g)
-        if stats is not None:
-            y._simclr_stats = (stats, M // bm)  # consumed by the next BatchNorm
+        res = run_igemm(ops, xn, w, y.permute(0, 2, 3, 1), g, want_stats=emit_stats)
+        if res is not None:
+            y._simclr_stats = res  # (partials, nblk): consumed by the next BatchNorm
         ctx.save_for_backward(x, weight)
         ctx.geom = (N, H, W, Cx, Ci, OH, OW, KH, KW, stride, pad, Co)
         return y
@@ -102,15 +159,12 @@ class ConvHipFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             g = fwd_geom(N, H, W, Cx, OH, OW, KH, KW, stride, pad, Co)
-            splits = ops.wgrad_splits(g)
-            K = KH * KW * Cx
-            partial = torch.empty((splits * Co * K,), device=dy.device, dtype=torch.float32)
             slot = getattr(weight, "_slot", None)
             if slot is not None:
                 out = slot.grad  # [Co, KH, KW, Ci] fp32 contiguous view into the flat buffer
             else:
                 out = torch.empty((Co, KH, KW, Ci), device=dy.device, dtype=torch.float32)
-            ops.wgrad(dyn, _nhwc(x), partial, out, g, splits, Ci, 0.0)
+            run_wgrad(ops, dyn, _nhwc(x), out, g, Ci)
             if slot is not None:
                 slot.store.mark_ready(slot.index)
             else:
@@ -131,7 +185,7 @@ def conv_dgrad(ops, dyn, w_ohwi, N, H, W, Ci, OH, OW, KH, KW, stride, pad, Co):
         ops.weight_transform(w_ohwi, wt, [Co, KH, KW, Ci, KH, KW, KH - 1, -1, KW - 1, -1])
         g = [N, OH, OW, Co, H, W, KH, KW, 1, 1, 1, 1, -(KH - 1 - pad), -(KW - 1 - pad), Ci,
              H, W, 1, 1, 0, 0, Ci]
-        ops.igemm(dyn, wt, dxn, None, None, g)
+        run_igemm(ops, dyn, wt, dxn, g)
         return dx
     assert stride == 2, "only stride 1/2 convolutions are supported"
     classes = []
@@ -155,7 +209,7 @@ def conv_dgrad(ops, dyn, w_ohwi, N, H, W, Ci, OH, OW, KH, KW, stride, pad, Co):
         iw0 = (c + pad - kw0) // 2
         g = [N, OH, OW, Co, ohc, owc, nkh, nkw, 1, 1, -1, -1, ih0, iw0, Ci,
              H, W, 2, 2, r, c, Ci]
-        ops.igemm(dyn, wt, dxn, None, None, g)
+        run_igemm(ops, dyn, wt, dxn, g)
     return dx
 
 

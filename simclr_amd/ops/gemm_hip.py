@@ -10,6 +10,7 @@ from typing import Optional
 import torch
 
 from . import _ext
+from .conv_hip import run_igemm, run_wgrad
 
 
 def _geom(M, K, N):
@@ -32,14 +33,10 @@ class LinearHipFn(torch.autograd.Function):
         xc = x.contiguous()
         w = _weight_bf16(weight)
         y = torch.empty((M, N), device=x.device, dtype=torch.bfloat16)
-        stats = None
-        bm = ops.igemm_bm(N)
-        if emit_stats and M % bm == 0:
-            stats = torch.empty(((M // bm) * 2 * N,), device=x.device, dtype=torch.float32)
         b = bias.detach().float().contiguous() if bias is not None else None
-        ops.igemm(xc, w, y, b, stats, _geom(M, K, N))
-        if stats is not None:
-            y._simclr_stats = (stats, M // bm)
+        res = run_igemm(ops, xc, w, y, _geom(M, K, N), bias=b, want_stats=emit_stats)
+        if res is not None:
+            y._simclr_stats = res
         ctx.save_for_backward(xc, weight, bias)
         return y
 
@@ -57,16 +54,14 @@ class LinearHipFn(torch.autograd.Function):
             wt = torch.empty((K, N), device=dy.device, dtype=torch.bfloat16)
             ops.weight_transform(_weight_bf16(weight), wt, [N, 1, 1, K, 1, 1, 0, 1, 0, 1])
             dx = torch.empty((M, K), device=dy.device, dtype=torch.bfloat16)
-            ops.igemm(dyc, wt, dx, None, None, _geom(M, N, K))
+            run_igemm(ops, dyc, wt, dx, _geom(M, N, K))
         dw = db = None
         if ctx.needs_input_grad[1]:
             g = _geom(M, K, N)
-            splits = ops.wgrad_splits(g)
-            partial = torch.empty((splits * N * K,), device=dy.device, dtype=torch.float32)
             slot = getattr(weight, "_slot", None)
             out = slot.grad if slot is not None else torch.empty(
                 (N, K), device=dy.device, dtype=torch.float32)
-            ops.wgrad(dyc, x, partial, out, g, splits, K, 0.0)
+            run_wgrad(ops, dyc, x, out, g, K)
             if slot is not None:
                 slot.store.mark_ready(slot.index)
             else:

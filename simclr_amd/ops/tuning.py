@@ -1,0 +1,51 @@
+"""Per-shape kernel-variant autotuning (tile shape of the implicit-GEMM kernels).
+
+The first time a problem shape is seen in eager mode every admissible tile variant is timed
+with HIP events (3 launches after 1 warm-up) and the fastest is cached for the process; inside a
+hipGraph capture, or with ``SIMCLR_AUTOTUNE=0``, the cached (else default) variant is used.
+Tuning launches write only to scratch outputs, so it has no side effects.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, Hashable, Sequence
+
+import torch
+
+_CACHE: Dict[Hashable, int] = {}
+ENABLED = os.environ.get("SIMCLR_AUTOTUNE", "1") != "0"
+
+
+def cached(key: Hashable):
+    return _CACHE.get(key)
+
+
+def pick(key: Hashable, candidates: Sequence[int], default: int,
+         run: Callable[[int], None], reps: int = 3) -> int:
+    if key in _CACHE:
+        return _CACHE[key]
+    cands = list(candidates)
+    if not cands:
+        return default
+    if (not ENABLED or len(cands) == 1 or not torch.cuda.is_available()
+            or torch.cuda.is_current_stream_capturing()):
+        return default if default in cands else cands[0]
+    best, best_t = cands[0], float("inf")
+    for v in cands:
+        run(v)
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            run(v)
+        e.record()
+        e.synchronize()
+        t = s.elapsed_time(e)
+        if t < best_t:
+            best, best_t = v, t
+    _CACHE[key] = best
+    return best
+
+
+def table() -> Dict[Hashable, int]:
+    return dict(_CACHE)

@@ -240,3 +240,53 @@ def test_augment_plain_mode(ops):
     ops.augment(imgs, None, 4, 1, 32, 32, 8, 0.5, 0, 0, 0, 0, out, None)
     ref = imgs.float() / 255
     assert torch.allclose(out.float()[..., :3], ref, atol=4e-3)
+
+
+@pytest.mark.parametrize("k,s,p", [(1, 1, 0), (3, 1, 1), (3, 2, 1)])
+def test_igemm_variants_prologue_epilogue(ops, k, s, p):
+    """Every tile variant, with the fused BN-apply prologue and both epilogue modes, against an
+    fp32 torch reference; and the wgrad kernel variants with the prologue."""
+    from simclr_amd.ops.conv_hip import fwd_geom
+    torch.manual_seed(7)
+    N, C, H, W, Co = 8, 64, 16, 16, 128
+    S = 2
+    x = _bf(torch.randn(N, C, H, W, device=DEV))
+    sc = (torch.rand(S, C, device=DEV) + 0.5).contiguous()
+    sh = (torch.randn(S, C, device=DEV) * 0.3).contiguous()
+    seg = torch.arange(N, device=DEV) // (N // S)
+    a = torch.relu(x.float() * sc[seg][:, :, None, None] + sh[seg][:, :, None, None])
+    a = _bf(a).float()
+    w = _bf(torch.randn(Co, C, k, k, device=DEV) / (C * k * k) ** 0.5)
+    ref = F.conv2d(a, w.float(), None, s, p)
+    OH, OW = ref.shape[-2:]
+    M = N * OH * OW
+    g = fwd_geom(N, H, W, C, OH, OW, k, k, s, p, Co)
+    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    wo = w.permute(0, 2, 3, 1).contiguous()
+    r = _bf(torch.randn(N, OH, OW, Co, device=DEV))
+    yy = _bf(torch.randn(N, OH, OW, Co, device=DEV))
+    refn = ref.permute(0, 2, 3, 1)
+    for v in range(ops.igemm_nvariants()):
+        bm = ops.igemm_variant_bm(v)
+        if (M // S) % bm:
+            continue
+        out = torch.empty(N, OH, OW, Co, device=DEV, dtype=torch.bfloat16)
+        ops.igemm(xn, wo, out, None, None, g, sc, sh, M // S, True, 0, None, None, v)
+        assert _rel(out, refn) < 1e-2, v
+        ops.igemm(xn, wo, out, None, None, g, sc, sh, M // S, True, 1, r, None, v)
+        assert _rel(out, refn + r.float()) < 1e-2, v
+        ops.igemm(xn, wo, out, None, None, g, sc, sh, M // S, True, 2, r, yy, v)
+        assert _rel(out, refn + torch.where(yy.float() > 0, r.float(), 0.0)) < 1e-2, v
+    # wgrad with the same prologue
+    wr = w.float().clone().requires_grad_(True)
+    yref = F.conv2d(a, wr, None, s, p)
+    gy = _bf(torch.randn_like(yref))
+    yref.backward(gy.float())
+    dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    for v in range(ops.wgrad_nvariants()):
+        splits = ops.wgrad_splits(g, v)
+        K = k * k * C
+        part = torch.empty(splits * Co * K, device=DEV)
+        out = torch.empty(Co, k, k, C, device=DEV)
+        ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, sc, sh, M // S, True, S, v)
+        assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, v
