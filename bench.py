@@ -38,12 +38,15 @@ def _init():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        idx = local % torch.cuda.device_count()
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        be = "nccl" if dev.type == "cuda" else "gloo"
+        # SIMCLR_DIST_BACKEND=gloo rehearses the multi-rank HIP path on one GPU (RCCL refuses
+        # two ranks on the same device); the driver's runs use nccl (= RCCL over xGMI).
+        be = os.environ.get("SIMCLR_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
         kw = {"device_id": dev} if be == "nccl" else {}
         dist.init_process_group(be, rank=rank, world_size=world, **kw)
     return rank, world, local, dev
@@ -152,12 +155,15 @@ def main(argv=None):
     ap.add_argument("--size", type=int, default=32)
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--gather", action="store_true", help="global negatives (all-gather of z)")
-    ap.add_argument("--graph", action="store_true", default=True)
+    ap.add_argument("--graph", action="store_true", default=None,
+                    help="capture the step in a hipGraph (default: on for 1 GPU, off for N>1)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--bucket-mb", dest="bucket_mb", type=float, default=32.0)
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     args = ap.parse_args(argv)
     rank, world, local, dev = _init()
+    if args.graph is None:
+        args.graph = world == 1
     if args.impl == "ours":
         dt, loss = run_ours(args, rank, world, dev)
     else:
