@@ -86,9 +86,10 @@ ConvFusion fusion_from(const c10::optional<Tensor>& pro_sc, const c10::optional<
   f.epi_mode = (int)epi_mode;
   f.epi_a = optbf(epi_a, "epi_a");
   f.epi_b = optbf(epi_b, "epi_b");
-  TORCH_CHECK(epi_mode >= 0 && epi_mode <= 2, "epi_mode");
-  if (epi_mode >= 1) TORCH_CHECK(f.epi_a && epi_a->numel() >= out_numel, "epilogue operand a");
-  if (epi_mode == 2) TORCH_CHECK(f.epi_b && epi_b->numel() >= out_numel, "epilogue operand b");
+  TORCH_CHECK(epi_mode >= 0 && epi_mode <= 4, "epi_mode");
+  if (epi_mode == 1 || epi_mode == 2 || epi_mode == 4)
+    TORCH_CHECK(f.epi_a && epi_a->numel() >= out_numel, "epilogue operand a");
+  if (epi_mode >= 2) TORCH_CHECK(f.epi_b && epi_b->numel() >= out_numel, "epilogue operand b");
   return f;
 }
 
@@ -97,7 +98,9 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
            int64_t pro_seg_rows, bool pro_relu, int64_t epi_mode,
            const c10::optional<Tensor>& epi_a, const c10::optional<Tensor>& epi_b,
-           int64_t variant) {
+           int64_t variant, const c10::optional<Tensor>& epi_ss,
+           const c10::optional<Tensor>& epi_mi, int64_t seg_rows, int64_t stats_seg_blocks,
+           int64_t stats_base, const c10::optional<Tensor>& epi_c) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -110,10 +113,42 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int bm = igemm_variant_bm((int)variant);
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
-  if (stats.has_value() && stats->defined())
+  const bool has_stats = stats.has_value() && stats->defined();
+  if (has_stats && stats_seg_blocks == 0)
     TORCH_CHECK(stats->numel() >= ((M + bm - 1) / bm) * 2 * g.N, "igemm: stats buffer too small");
-  ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, 2, epi_mode, epi_a, epi_b,
+  ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, 1, epi_mode, epi_a, epi_b,
                              g.C, out.numel());
+  f.seg_rows = (int)seg_rows;
+  f.stats_seg_blocks = (int)stats_seg_blocks;
+  f.stats_base = (int)stats_base;
+  if (seg_rows > 0)
+    TORCH_CHECK(seg_rows % bm == 0 && M % seg_rows == 0,
+                "igemm: segment rows must be a multiple of the tile rows and divide M");
+  if (stats_seg_blocks > 0) {
+    TORCH_CHECK(has_stats && seg_rows > 0, "igemm: stats remap needs stats and seg_rows");
+    const int64_t nseg = M / seg_rows;
+    TORCH_CHECK(stats_base >= 0 && stats_base + seg_rows / bm <= stats_seg_blocks,
+                "igemm: stats remap window out of range");
+    TORCH_CHECK(stats->numel() >= nseg * stats_seg_blocks * 2 * g.N,
+                "igemm: remapped stats buffer too small");
+  }
+  if (epi_mode == 3 || epi_mode == 4) {
+    TORCH_CHECK(seg_rows > 0, "igemm mode 3/4 needs seg_rows");
+    TORCH_CHECK(!f.pro_sc || epi_mode == 3, "igemm: no prologue with epilogue mode 4");
+    const int64_t nseg = M / seg_rows;
+    f.epi_mi = optf32(epi_mi, "epi_mi");
+    f.epi_S = (int)nseg;
+    TORCH_CHECK(f.epi_mi && epi_mi->numel() >= 2 * nseg * g.N,
+                "igemm mode 3/4: mean/invstd table must be [2][S][N]");
+    if (epi_mode == 3) {
+      f.epi_ss = optf32(epi_ss, "epi_ss");
+      TORCH_CHECK(f.epi_ss && epi_ss->numel() >= 2 * nseg * g.N,
+                  "igemm mode 3: scale/shift table must be [2][S][N]");
+    } else {
+      f.epi_c = optbf(epi_c, "epi_c");
+      TORCH_CHECK(f.epi_c && epi_c->numel() >= out.numel(), "igemm mode 4: epilogue operand c");
+    }
+  }
   if (f.pro_sc) {
     TORCH_CHECK(pro_seg_rows > 0 && pro_seg_rows % bm == 0 && M % pro_seg_rows == 0,
                 "igemm prologue: segment rows must be a multiple of the tile rows");
@@ -209,7 +244,11 @@ void bn_reduce(const Tensor& partial, int64_t nblk, int64_t S, int64_t C, const 
 
 void bn_final(const Tensor& stats, int64_t S, int64_t C, double count, double eps, double momentum,
               const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv, const Tensor& mi,
-              const c10::optional<Tensor>& nbt) {
+              const c10::optional<Tensor>& nbt, const c10::optional<Tensor>& gamma,
+              const c10::optional<Tensor>& beta, const c10::optional<Tensor>& ss) {
+  if (ss.has_value() && ss->defined()) TORCH_CHECK(ss->numel() >= 2 * S * C, "bn_finalize: ss size");
+  if (gamma.has_value() && gamma->defined()) TORCH_CHECK(gamma->numel() == C, "bn_finalize: gamma");
+  if (beta.has_value() && beta->defined()) TORCH_CHECK(beta->numel() == C, "bn_finalize: beta");
   TORCH_CHECK(stats.numel() >= 2 * S * C && mi.numel() >= 2 * S * C, "bn_finalize sizes");
   int64_t* nb = nullptr;
   if (nbt.has_value() && nbt->defined()) {
@@ -218,7 +257,21 @@ void bn_final(const Tensor& stats, int64_t S, int64_t C, double count, double ep
   }
   bn_finalize(f32(stats, "stats"), S, C, (float)count, (float)eps, (float)momentum,
               optf32w(rm, "running_mean"), optf32w(rv, "running_var"), f32w(mi, "mean_invstd"), nb,
-              cur_stream());
+              optf32(gamma, "gamma"), optf32(beta, "beta"), optf32w(ss, "ss"), cur_stream());
+}
+
+void bn_apply_ss_op(const Tensor& x, const Tensor& ss, const c10::optional<Tensor>& res,
+                    const c10::optional<Tensor>& rss, const Tensor& y, int64_t S, bool relu) {
+  check_rc(x, S, "bn_apply_ss");
+  const int C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(y.numel() == x.numel(), "bn_apply_ss: y size");
+  TORCH_CHECK(ss.numel() >= 2 * S * C, "bn_apply_ss: ss size");
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) TORCH_CHECK(res->numel() == x.numel(), "bn_apply_ss: res size");
+  if (rss.has_value() && rss->defined())
+    TORCH_CHECK(has_res && rss->numel() >= 2 * S * C, "bn_apply_ss: rss needs res, [2][S][C]");
+  bn_apply_ss(bf(x, "x"), f32(ss, "ss"), optbf(res, "res"), optf32(rss, "rss"), bfw(y, "y"), R, C,
+              S, relu ? 1 : 0, cur_stream());
 }
 
 void bn_apply_op(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& y,
@@ -417,7 +470,7 @@ void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int6
 }  // namespace
 
 TORCH_LIBRARY(simclr_amd, m) {
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None) -> ()", &igemm);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
   m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);
@@ -429,7 +482,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_blocks(int R, int C, int S) -> int", &bn_blocks);
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
-  m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt) -> ()", &bn_final);
+  m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
+  m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);
   m.def("bn_bwd_reduce(Tensor dy, Tensor? y, Tensor x, Tensor mi, int S, bool relu, Tensor(a!) partial) -> ()", &bn_bwd_reduce_op);

@@ -126,9 +126,11 @@ __global__ void k_reduce_partials(const float* __restrict__ partial, int nblk, i
 }
 
 // stats [2][S][C] -> mean_invstd [2][S][C]; sequential running-stat updates per segment
+// Optionally also the fused-apply table ss [2][S][C]: scale = γ·invstd, shift = β − mean·scale.
 __global__ void k_bn_finalize(const float* __restrict__ stats, int S, int C, float count, float eps,
                               float momentum, float* running_mean, float* running_var,
-                              float* __restrict__ mi, int64_t* nbt) {
+                              float* __restrict__ mi, int64_t* nbt, const float* __restrict__ gamma,
+                              const float* __restrict__ beta, float* __restrict__ ss) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt != nullptr) nbt[0] += S;  // num_batches_tracked: one per view
   if (c >= C) return;
@@ -139,8 +141,14 @@ __global__ void k_bn_finalize(const float* __restrict__ stats, int S, int C, flo
     const float mean = stats[s * C + c] / count;
     float var = stats[S * C + s * C + c] / count - mean * mean;
     var = var > 0.f ? var : 0.f;
+    const float inv = rsqrtf(var + eps);
     mi[s * C + c] = mean;
-    mi[S * C + s * C + c] = rsqrtf(var + eps);
+    mi[S * C + s * C + c] = inv;
+    if (ss != nullptr) {
+      const float sc = (gamma ? gamma[c] : 1.f) * inv;
+      ss[s * C + c] = sc;
+      ss[S * C + s * C + c] = (beta ? beta[c] : 0.f) - mean * sc;
+    }
     rm = (1.f - momentum) * rm + momentum * mean;
     rv = (1.f - momentum) * rv + momentum * var * unbias;
   }
@@ -209,6 +217,78 @@ __global__ __launch_bounds__(256) void k_bn_apply(const uint16_t* __restrict__ x
           for (int e = 0; e < 4; ++e) {
             o[2 * e] += lo_bf(rv[u][e]);
             o[2 * e + 1] += hi_bf(rv[u][e]);
+          }
+        }
+        if (relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], 0.f);
+        }
+        u32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = pack2bf(o[2 * e], o[2 * e + 1]);
+        *(u32x4*)(y + sbase + (size_t)r * C + cc * 8) = w;
+      }
+    }
+  }
+}
+
+// y = relu?(x·sc + sh [+ res | + res·rsc + rsh]) with precomputed [2][S][C] tables: the
+// block-output apply of the fused ResNet executor (BN3 + downsample-BN + residual + ReLU in one
+// pass; neither BN output is materialised separately).
+template <int RES>  // 0 none, 1 plain residual, 2 affine residual
+__global__ __launch_bounds__(256) void k_bn_apply_ss(const uint16_t* __restrict__ x,
+                                                     const float* __restrict__ ss,
+                                                     const uint16_t* __restrict__ res,
+                                                     const float* __restrict__ rss,
+                                                     uint16_t* __restrict__ y, int R, int C, int S,
+                                                     int relu) {
+  const int CH = C / 8;
+  const int TPR = CH < 256 ? CH : 256;
+  const int RPB = 256 / TPR;
+  const int Rs = R / S;
+  const int seg = blockIdx.y;
+  const int cc0 = threadIdx.x % TPR;
+  const int rl = threadIdx.x / TPR;
+  if (rl >= RPB) return;
+  const size_t sbase = (size_t)seg * Rs * C;
+  const size_t sbytes = (size_t)Rs * C * 2;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x + sbase, sbytes);
+  const __amdgpu_buffer_rsrc_t rr = rsrc(RES ? res + sbase : x + sbase, sbytes);
+  for (int cc = cc0; cc < CH; cc += TPR) {
+    float sc[8], sh[8], rsc[8], rsh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = cc * 8 + e;
+      sc[e] = ss[seg * C + c];
+      sh[e] = ss[(S + seg) * C + c];
+      if (RES == 2) {
+        rsc[e] = rss[seg * C + c];
+        rsh[e] = rss[(S + seg) * C + c];
+      }
+    }
+    for (int r0 = blockIdx.x * RPB * UNR + rl; r0 < Rs; r0 += gridDim.x * RPB * UNR) {
+      u32x4 v[UNR], rv[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const uint32_t off = (uint32_t)(((size_t)(r0 + u * RPB) * C + cc * 8) * 2);
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+        if (RES) rv[u] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * RPB;
+        if (r >= Rs) break;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[2 * e] = lo_bf(v[u][e]) * sc[2 * e] + sh[2 * e];
+          o[2 * e + 1] = hi_bf(v[u][e]) * sc[2 * e + 1] + sh[2 * e + 1];
+          if (RES == 1) {
+            o[2 * e] += lo_bf(rv[u][e]);
+            o[2 * e + 1] += hi_bf(rv[u][e]);
+          } else if (RES == 2) {
+            o[2 * e] += lo_bf(rv[u][e]) * rsc[2 * e] + rsh[2 * e];
+            o[2 * e + 1] += hi_bf(rv[u][e]) * rsc[2 * e + 1] + rsh[2 * e + 1];
           }
         }
         if (relu) {
@@ -497,9 +577,22 @@ void bn_reduce_partials(const float* partial, int nblk, int S, int C, float* sta
 
 void bn_finalize(const float* stats, int S, int C, float count, float eps, float momentum,
                  float* running_mean, float* running_var, float* mean_invstd, int64_t* nbt,
-                 hipStream_t s) {
+                 const float* gamma, const float* beta, float* scale_shift, hipStream_t s) {
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, stats, S, C, count, eps,
-                     momentum, running_mean, running_var, mean_invstd, nbt);
+                     momentum, running_mean, running_var, mean_invstd, nbt, gamma, beta,
+                     scale_shift);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_apply_ss(const uint16_t* x, const float* ss, const uint16_t* res, const float* rss,
+                 uint16_t* y, int R, int C, int S, int relu, hipStream_t s) {
+  const dim3 grid(apply_grid(R, C, S), S);
+  if (res == nullptr)
+    hipLaunchKernelGGL(k_bn_apply_ss<0>, grid, dim3(256), 0, s, x, ss, res, rss, y, R, C, S, relu);
+  else if (rss == nullptr)
+    hipLaunchKernelGGL(k_bn_apply_ss<1>, grid, dim3(256), 0, s, x, ss, res, rss, y, R, C, S, relu);
+  else
+    hipLaunchKernelGGL(k_bn_apply_ss<2>, grid, dim3(256), 0, s, x, ss, res, rss, y, R, C, S, relu);
   HIP_CHECK_LAUNCH();
 }
 

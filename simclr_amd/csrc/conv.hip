@@ -47,10 +47,23 @@ struct IgemmArgs {
   const float* pro_sc;
   const float* pro_sh;
   int pro_seg_rows, pro_relu;
-  // epilogue: 0 store, 1 out = acc + epi_a, 2 out = acc + (epi_b > 0 ? epi_a : 0)
+  // epilogue: 0 store, 1 out = acc + epi_a, 2 out = acc + (epi_b > 0 ? epi_a : 0),
+  // 3 out = g = (epi_b*sc + sh > 0) ? acc : 0 with BatchNorm-backward partials Σg, Σg·x̂
+  //   (x̂ = (epi_b - mean)·invstd) in place of Σy, Σy² (ReLU mask + BN bwd reduce of the
+  //   producing layer, fused into the dgrad that computes its output gradient)
+  // 4 v = acc + epi_a; out = g = (epi_b > 0) ? v : 0 with partials Σg, Σg·x̂ (x̂ from epi_c):
+  //   the block-input gradient of a residual block, already masked by the previous block's
+  //   output ReLU, with that block's last-BN backward reduce folded in
   int epi_mode;
   const uint16_t* epi_a;
   const uint16_t* epi_b;
+  const uint16_t* epi_c;
+  const float* epi_ss;  // mode 3: [2][S][N] BN scale / shift
+  const float* epi_mi;  // mode 3/4: [2][S][N] BN mean / invstd
+  int epi_S;
+  // stats row remap (segment-major partials when one BN's rows span several launches):
+  //   blk = seg * stats_seg_blocks + stats_base + (m0 - seg * seg_rows) / BM, seg = m0 / seg_rows
+  int seg_rows, stats_seg_blocks, stats_base;
 };
 
 __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const float* sh, bool ok,
@@ -69,7 +82,7 @@ __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const fl
   return w;
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool PRO, int EPI>
 __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -120,7 +133,7 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
   u32x4 ra[ACH], rb[BCH];
   bool rok[ACH];
   float psc[8], psh[8];
-  const bool pro = p.pro_sc != nullptr;
+  constexpr bool pro = PRO;
   const int pseg = pro ? m0 / p.pro_seg_rows : 0;  // block-uniform (host guarantees)
   const uint32_t OOB_A = p.a_bytes, OOB_B = p.b_bytes;
 
@@ -237,6 +250,21 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
   const int n = n0 + ch * 8;
+  const int seg = p.seg_rows > 0 ? m0 / p.seg_rows : 0;  // block-uniform (host guarantees)
+  float esc[8], esh[8], emu[8], einv[8];
+  if (EPI == 3 || EPI == 4) {
+    const int S = p.epi_S;
+    const int cb = n < p.N ? n : 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (EPI == 3) {
+        esc[e] = p.epi_ss[seg * p.N + cb + e];
+        esh[e] = p.epi_ss[(S + seg) * p.N + cb + e];
+      }
+      emu[e] = p.epi_mi[seg * p.N + cb + e];
+      einv[e] = p.epi_mi[(S + seg) * p.N + cb + e];
+    }
+  }
   for (int row = r0; row < BM; row += RSTEP) {
     const int m = m0 + row;
     if (m >= p.M || n >= p.N) continue;
@@ -251,12 +279,12 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
       const int ow = rem - oh * p.OW;
       o = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
     }
-    if (p.epi_mode == 1) {
+    if (EPI == 1) {
       const u32x4 r = *(const u32x4*)(p.epi_a + o);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         v[e] = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
-    } else if (p.epi_mode == 2) {
+    } else if (EPI == 2) {
       const u32x4 d = *(const u32x4*)(p.epi_a + o);
       const u32x4 y = *(const u32x4*)(p.epi_b + o);
 #pragma unroll
@@ -265,9 +293,38 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
         const float b = hi_bf(y[e]) > 0.f ? hi_bf(d[e]) : 0.f;
         v[e] = pack2bf(lo_bf(v[e]) + a, hi_bf(v[e]) + b);
       }
+    } else if (EPI == 3) {
+      const u32x4 y = *(const u32x4*)(p.epi_b + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y0 = lo_bf(y[e]), y1 = hi_bf(y[e]);
+        const float g0 = y0 * esc[2 * e] + esh[2 * e] > 0.f ? lo_bf(v[e]) : 0.f;
+        const float g1 = y1 * esc[2 * e + 1] + esh[2 * e + 1] > 0.f ? hi_bf(v[e]) : 0.f;
+        v[e] = pack2bf(g0, g1);  // exact: g is 0 or an already-rounded bf16 value
+        if (p.stats != nullptr) {
+          s1[2 * e] += g0; s2[2 * e] += g0 * ((y0 - emu[2 * e]) * einv[2 * e]);
+          s1[2 * e + 1] += g1; s2[2 * e + 1] += g1 * ((y1 - emu[2 * e + 1]) * einv[2 * e + 1]);
+        }
+      }
+    } else if (EPI == 4) {
+      const u32x4 r = *(const u32x4*)(p.epi_a + o);
+      const u32x4 y = *(const u32x4*)(p.epi_b + o);
+      const u32x4 xa = *(const u32x4*)(p.epi_c + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t sum = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
+        const float g0 = lo_bf(y[e]) > 0.f ? lo_bf(sum) : 0.f;
+        const float g1 = hi_bf(y[e]) > 0.f ? hi_bf(sum) : 0.f;
+        v[e] = pack2bf(g0, g1);
+        if (p.stats != nullptr) {
+          s1[2 * e] += g0; s2[2 * e] += g0 * ((lo_bf(xa[e]) - emu[2 * e]) * einv[2 * e]);
+          s1[2 * e + 1] += g1;
+          s2[2 * e + 1] += g1 * ((hi_bf(xa[e]) - emu[2 * e + 1]) * einv[2 * e + 1]);
+        }
+      }
     }
     *(u32x4*)(p.out + o) = v;
-    if (p.stats != nullptr) {
+    if (EPI != 3 && EPI != 4 && p.stats != nullptr) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float a = lo_bf(v[e]), b = hi_bf(v[e]);
@@ -291,8 +348,11 @@ __global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
         a += red[(r * BN + tid) * 2 + 0];
         b += red[(r * BN + tid) * 2 + 1];
       }
-      p.stats[((size_t)mb * 2 + 0) * p.N + n0 + tid] = a;
-      p.stats[((size_t)mb * 2 + 1) * p.N + n0 + tid] = b;
+      const int blk = p.stats_seg_blocks > 0
+                          ? seg * p.stats_seg_blocks + p.stats_base + (m0 - seg * p.seg_rows) / BM
+                          : mb;
+      p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
+      p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
     }
   }
 }
@@ -313,7 +373,7 @@ struct WgradArgs {
   int pro_seg_rows, pro_relu, pro_S;
 };
 
-template <int BCO, int BKK, int WM, int WN>
+template <int BCO, int BKK, int WM, int WN, bool PRO>
 __global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
   constexpr int FM = TCO / 16, FN = TKK / 16;
@@ -357,7 +417,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
   u32x4 rd[DCH], rx[XCH];
   bool xok[XCH];
   bool xseg[XCH];
-  const bool pro = p.pro_sc != nullptr;
+  constexpr bool pro = PRO;
   float psc0[8], psh0[8], psc1[8], psh1[8];
   if (pro) {
     const int cc = k_ok ? ci : 0;
@@ -530,8 +590,8 @@ __global__ void weight_transform(const uint16_t* __restrict__ W, uint16_t* __res
   }
 }
 
-template <int BM, int BN, int WM, int WN>
-void launch_igemm(const IgemmArgs& a0, hipStream_t s) {
+template <int BM, int BN, int WM, int WN, bool PRO, int EPI>
+void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   IgemmArgs a = a0;
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
@@ -541,18 +601,43 @@ void launch_igemm(const IgemmArgs& a0, hipStream_t s) {
   const size_t red = (size_t)(256 / (BN / 8)) * BN * 2 * 4;
   if (cst > lds) lds = cst;
   if (red > lds) lds = red;
-  hipLaunchKernelGGL((igemm_nt<BM, BN, WM, WN>), dim3(grid), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((igemm_nt<BM, BN, WM, WN, PRO, EPI>), dim3(grid), dim3(256), lds, s, a);
   HIP_CHECK_LAUNCH();
+}
+
+// compile-time fusion modes (prologue x epilogue), so each launch carries only its own work
+template <int BM, int BN, int WM, int WN>
+void launch_igemm(const IgemmArgs& a, hipStream_t s) {
+  if (a.pro_sc != nullptr) {
+    switch (a.epi_mode) {
+      case 1: launch_igemm_t<BM, BN, WM, WN, true, 1>(a, s); break;
+      case 2: launch_igemm_t<BM, BN, WM, WN, true, 2>(a, s); break;
+      case 3: launch_igemm_t<BM, BN, WM, WN, true, 3>(a, s); break;
+      default: launch_igemm_t<BM, BN, WM, WN, true, 0>(a, s); break;
+    }
+    return;
+  }
+  switch (a.epi_mode) {
+    case 1: launch_igemm_t<BM, BN, WM, WN, false, 1>(a, s); break;
+    case 2: launch_igemm_t<BM, BN, WM, WN, false, 2>(a, s); break;
+    case 3: launch_igemm_t<BM, BN, WM, WN, false, 3>(a, s); break;
+    case 4: launch_igemm_t<BM, BN, WM, WN, false, 4>(a, s); break;
+    default: launch_igemm_t<BM, BN, WM, WN, false, 0>(a, s); break;
+  }
 }
 
 template <int BCO, int BKK, int WM, int WN>
 void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
+  const bool pro = a0.pro_sc != nullptr;
   WgradArgs a = a0;
   a.nCo = (a.N + BCO - 1) / BCO;
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
   const size_t lds = (size_t)2 * 64 * ((BCO + 8) + (BKK + 8)) * 2;
-  hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN>), dim3(grid), dim3(256), lds, s, a);
+  if (pro)
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true>), dim3(grid), dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false>), dim3(grid), dim3(256), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -585,7 +670,9 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.b_bytes = (uint32_t)((size_t)a.N * a.K * 2);
   a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh; a.pro_seg_rows = f.pro_seg_rows > 0 ? f.pro_seg_rows : a.M;
   a.pro_relu = f.pro_relu;
-  a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b;
+  a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b; a.epi_c = f.epi_c;
+  a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
+  a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
   switch (variant) {
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;

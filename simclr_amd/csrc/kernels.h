@@ -24,9 +24,18 @@ struct ConvFusion {
   int pro_seg_rows = 0;           // rows per segment (BM must divide it for igemm)
   int pro_relu = 0;
   int pro_S = 1;
-  int epi_mode = 0;               // igemm: 1 out = acc + a; 2 out = acc + (b > 0 ? a : 0)
+  int epi_mode = 0;               // igemm: 1 out = acc + a; 2 out = acc + (b > 0 ? a : 0);
+                                  // 3 out = (b*sc+sh > 0 ? acc : 0) + BN-bwd partials
+                                  // 4 out = (b > 0 ? acc + a : 0) + BN-bwd partials vs c
   const uint16_t* epi_a = nullptr;
   const uint16_t* epi_b = nullptr;
+  const uint16_t* epi_c = nullptr;  // mode 4: pre-BN activation for x̂
+  const float* epi_ss = nullptr;  // mode 3: [2][S][N] scale/shift
+  const float* epi_mi = nullptr;  // mode 3/4: [2][S][N] mean/invstd
+  int epi_S = 1;
+  int seg_rows = 0;               // rows per segment of the output (stats remap, mode 3)
+  int stats_seg_blocks = 0;       // >0: segment-major stats rows (see conv.hip)
+  int stats_base = 0;
 };
 int igemm_num_variants();
 int igemm_variant_bm(int v);
@@ -54,7 +63,10 @@ void bn_reduce_partials(const float* partial, int nblk_per_seg, int S, int C, fl
                         float* ws, hipStream_t s);
 void bn_finalize(const float* stats, int S, int C, float count, float eps, float momentum,
                  float* running_mean, float* running_var, float* mean_invstd, int64_t* nbt,
-                 hipStream_t s);
+                 const float* gamma, const float* beta, float* scale_shift, hipStream_t s);
+// y = relu?(x*sc + sh + [res | res*rsc + rsh]); ss / rss are [2][S][C] scale/shift tables
+void bn_apply_ss(const uint16_t* x, const float* ss, const uint16_t* res, const float* rss,
+                 uint16_t* y, int R, int C, int S, int relu, hipStream_t s);
 void bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* mean_invstd,
               const float* gamma, const float* beta, int R, int C, int S, int relu,
               hipStream_t s);

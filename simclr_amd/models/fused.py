@@ -1,0 +1,445 @@
+"""Fused residual-stage executor: the ResNet body (layer1..layer4) as ONE hand-scheduled
+forward/backward on the HIP kernels, instead of a chain of per-op autograd nodes.
+
+Reference semantics: torchvision BasicBlock / Bottleneck (v1.5) inside the reference's
+``ContrastiveModel.f`` (``/root/reference/model.py:76-114``) with every BatchNorm converted to
+SyncBatchNorm (main.py:176) and the two views run as separate forwards (main.py:112-113, so BN
+statistics are per view: SURVEY Q17).  The math is unchanged; what changes is where the
+BatchNorm work happens:
+
+forward, per block (S = 2 view segments, stats per segment, all-reduced across ranks)::
+
+    a1 = conv1(x)                      epilogue: Σ, Σ² partials of a1        (BN1 stats)
+    a2 = conv2(relu(bn1(a1)))          prologue applies BN1+ReLU on the gathered operand, so
+                                       the BN1 output is never written to HBM; epilogue: BN2 stats
+    a3 = conv3(relu(bn2(a2)))          (bottleneck only) same
+    ad = convd(x)                      (downsample) epilogue: BNd stats
+    out = relu(bn3(a3) + [bnd(ad) | x])  one elementwise pass (two affines + add + ReLU)
+
+backward, per block, given g = dL/d out::
+
+    BN3 (and BNd) backward reduce/apply with the ReLU mask of ``out`` → da3 (, dad, or the
+    identity-path gradient g3 = g·[out > 0])
+    db2 = dgrad3(da3): the epilogue applies the BN2-ReLU mask (recomputed from a2) and emits the
+          BN2 backward partials Σg, Σg·x̂ (no separate reduce pass) → finalize → da2 (one pass)
+    dW3 = wgrad(da3, relu(bn2(a2)))   prologue recomputes the BN2 output on the fly
+    ... same for conv2 / BN1 ...
+    dx  = dgrad1(da1) + [dgrad_d(dad) | g3]  accumulated in the dgrad epilogue (no extra add)
+
+Compared with the module path this removes the BN1/BN2 apply passes, both backward reduce
+passes of BN1/BN2, every autograd gradient-accumulation add at the residual branches, and the
+materialised BN outputs (less HBM traffic and memory).  Weight / BN-parameter gradients go
+straight into the flat fp32 gradient buffer and notify the bucketed all-reducer as soon as
+they are final (overlap with the rest of the backward).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+from ..ops.conv_hip import (fwd_geom, igemm_choose, igemm_launch, run_wgrad, shadow_ohwi)
+from ..parallel import state as pstate
+
+
+def _empty_nhwc(n, h, w, c, dev, dtype=torch.bfloat16):
+    return torch.empty((n, h, w, c), device=dev, dtype=dtype)
+
+
+def _allreduce(t: torch.Tensor, st) -> None:
+    if st.world_size > 1:
+        dist.all_reduce(t, group=st.group)
+
+
+def _deliver_grad(param: torch.Tensor, compute) -> None:
+    """Run ``compute(out)`` writing the fp32 gradient of ``param`` into its flat-store slot
+    (and notify the reducer); unbound parameters accumulate into ``param.grad``."""
+    slot = getattr(param, "_slot", None)
+    if slot is not None:
+        compute(slot.grad)
+        slot.store.mark_ready(slot.index)
+        return
+    g = torch.empty(param.shape if param.dim() != 4 else
+                    (param.shape[0], param.shape[2], param.shape[3], param.shape[1]),
+                    device=param.device, dtype=torch.float32)
+    compute(g)
+    if param.dim() == 4:
+        g = g.permute(0, 3, 1, 2)
+    if param.grad is None:
+        param.grad = g.contiguous() if param.dim() != 4 else g
+    else:
+        param.grad.add_(g)
+
+
+@dataclass
+class _ConvSpec:
+    conv: torch.nn.Module
+    bn: torch.nn.Module
+    stride: int
+    k: int
+    pad: int
+
+
+@dataclass
+class _BlockSpec:
+    convs: List[_ConvSpec]
+    down: Optional[_ConvSpec]
+
+
+@dataclass
+class _BNState:
+    mi: torch.Tensor        # [2][S][C] mean / invstd
+    ss: torch.Tensor        # [2][S][C] scale / shift
+    count: float
+
+
+@dataclass
+class _BlockTape:
+    x: torch.Tensor                     # block input, NHWC bf16
+    acts: List[torch.Tensor] = field(default_factory=list)   # pre-BN conv outputs (NHWC)
+    bns: List[_BNState] = field(default_factory=list)
+    # what conv i actually consumed: (tensor, prologue scale/shift or None)
+    ins: List[Tuple[torch.Tensor, Optional[torch.Tensor]]] = field(default_factory=list)
+    ad: Optional[torch.Tensor] = None
+    bnd: Optional[_BNState] = None
+    out: Optional[torch.Tensor] = None
+
+
+class FusedStages:
+    """Executor over ``resnet.layer1..layer4`` (modules stay the parameter / state owners)."""
+
+    def __init__(self, resnet: torch.nn.Module, segments: int = 2):
+        from .resnet import BasicBlock, Bottleneck
+        self.resnet = resnet
+        self.S = segments
+        self.calls = 0
+        self.blocks: List[_BlockSpec] = []
+        for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4):
+            for blk in layer:
+                if isinstance(blk, Bottleneck):
+                    convs = [_ConvSpec(blk.conv1, blk.bn1, 1, 1, 0),
+                             _ConvSpec(blk.conv2, blk.bn2, blk.stride, 3, 1),
+                             _ConvSpec(blk.conv3, blk.bn3, 1, 1, 0)]
+                elif isinstance(blk, BasicBlock):
+                    convs = [_ConvSpec(blk.conv1, blk.bn1, blk.stride, 3, 1),
+                             _ConvSpec(blk.conv2, blk.bn2, 1, 3, 1)]
+                else:
+                    raise TypeError(f"unsupported block {type(blk).__name__}")
+                down = None
+                if blk.downsample is not None:
+                    down = _ConvSpec(blk.downsample[0], blk.downsample[1], blk.stride, 1, 0)
+                self.blocks.append(_BlockSpec(convs, down))
+
+    # ------------------------------------------------------------------ feasibility
+    def supported(self, x: torch.Tensor) -> bool:
+        """Every fused launch needs view segments aligned to the smallest tile (64 rows)."""
+        if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4:
+            return False
+        Nb, C, H, W = x.shape
+        if Nb % self.S or H != W:
+            return False
+        n = Nb // self.S
+        for b in self.blocks:
+            hin = H
+            for i, cs in enumerate(b.convs):
+                oh = (hin + 2 * cs.pad - cs.k) // cs.stride + 1
+                if (n * oh * oh) % 64:
+                    return False
+                if cs.stride == 2:  # BN-epilogue dgrad: per parity-class segments
+                    for r in (0, 1):
+                        if (n * ((hin - r + 1) // 2) ** 2) % 64:
+                            return False
+                hin = oh
+            H = hin
+        return True
+
+    # ------------------------------------------------------------------ building blocks
+    def _conv_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int):
+        """a = conv(pro(x)) with BN statistics partials in the epilogue."""
+        Nb, H, W, C = xn.shape
+        Co = cs.conv.out_channels
+        OH = (H + 2 * cs.pad - cs.k) // cs.stride + 1
+        OW = (W + 2 * cs.pad - cs.k) // cs.stride + 1
+        w = shadow_ohwi(cs.conv.weight, C)
+        a = _empty_nhwc(Nb, OH, OW, Co, xn.device)
+        g = fwd_geom(Nb, H, W, C, OH, OW, cs.k, cs.k, cs.stride, cs.pad, Co)
+        M = Nb * OH * OW
+        pro = None
+        if pro_ss is not None:
+            pro = (pro_ss[0], pro_ss[1], M // S, True)
+        v = igemm_choose(ops, xn, w, a, g, want_stats=True, pro=pro, seg_rows=M // S)
+        bm = ops.igemm_variant_bm(v)
+        stats = torch.empty(((M // bm) * 2 * Co,), device=xn.device, dtype=torch.float32)
+        igemm_launch(ops, xn, w, a, g, v, stats=stats, pro=pro)
+        return a, stats, M // bm // S
+
+    def _bn_fwd(self, ops, bn, partial, nblk_seg: int, rows_seg: int, S: int, st) -> _BNState:
+        C = bn.num_features
+        dev = partial.device
+        stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        ops.bn_reduce(partial, nblk_seg, S, C, stats)
+        _allreduce(stats, st)
+        count = float(rows_seg * st.world_size)
+        mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        ss = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean, bn.running_var,
+                        mi, bn.num_batches_tracked, bn.weight.detach(), bn.bias.detach(), ss)
+        return _BNState(mi, ss.view(2, S * C), count)
+
+    def _bn_bwd(self, ops, bn, partial, nblk_seg: int, bs: _BNState, S: int, st) -> torch.Tensor:
+        """Finalize a BN backward from Σg, Σg·x̂ partials: dγ, dβ → flat grads; returns coef."""
+        C = bn.num_features
+        dev = partial.device
+        sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        ops.bn_reduce(partial, nblk_seg, S, C, sums)
+        _allreduce(sums, st)
+        coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
+        res = {}
+
+        def run(dg, db):
+            ops.bn_bwd_finalize(sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db, coef)
+
+        gslot = getattr(bn.weight, "_slot", None)
+        bslot = getattr(bn.bias, "_slot", None)
+        if gslot is not None and bslot is not None:
+            run(gslot.grad, bslot.grad)
+            gslot.store.mark_ready(gslot.index)
+            bslot.store.mark_ready(bslot.index)
+        else:
+            dg = torch.empty((C,), device=dev, dtype=torch.float32)
+            db = torch.empty((C,), device=dev, dtype=torch.float32)
+            run(dg, db)
+            _deliver_grad(bn.weight, lambda o: o.copy_(dg))
+            _deliver_grad(bn.bias, lambda o: o.copy_(db))
+        return coef
+
+    def _wgrad(self, ops, dyn, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int):
+        Nb, H, W, C = xn.shape
+        Co = cs.conv.out_channels
+        OH, OW = dyn.shape[1], dyn.shape[2]
+        g = fwd_geom(Nb, H, W, C, OH, OW, cs.k, cs.k, cs.stride, cs.pad, Co)
+        M = Nb * OH * OW
+        pro = None
+        if pro_ss is not None:
+            pro = (pro_ss[0], pro_ss[1], M // S, True, S)
+        _deliver_grad(cs.conv.weight, lambda out: run_wgrad(ops, dyn, xn, out, g, C, pro=pro))
+
+    def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
+               dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None):
+        """dx (NHWC) = conv-transpose(dy).  ``accumulate``: dx += result (dx must be given).
+
+        ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
+        (segment-major across stride-2 parity classes) → (dx, partial, blocks_per_segment):
+          ("mask", a_prev, bn_state)      mode 3: g = dx·[bn(a_prev) > 0] (BN+ReLU producer)
+          ("res", resid, y, a_prev, mi)   mode 4: g = (dx + resid)·[y > 0] (residual-block
+                                          producer: y = its output, a_prev = its last pre-BN
+                                          activation); resid may alias dx (in-place add)
+        """
+        Nb, H, W, Ci = in_shape
+        _, OH, OW, Co = dyn.shape
+        KH = KW = cs.k
+        dev = dyn.device
+        w = shadow_ohwi(cs.conv.weight, Ci)
+        if dx is None:
+            dx = _empty_nhwc(Nb, H, W, Ci, dev)
+        launches = []
+        if cs.stride == 1:
+            wt = torch.empty((Ci, KH, KW, Co), device=dev, dtype=torch.bfloat16)
+            ops.weight_transform(w, wt, [Co, KH, KW, Ci, KH, KW, KH - 1, -1, KW - 1, -1])
+            g = [Nb, OH, OW, Co, H, W, KH, KW, 1, 1, 1, 1, -(KH - 1 - cs.pad),
+                 -(KW - 1 - cs.pad), Ci, H, W, 1, 1, 0, 0, Ci]
+            launches.append((wt, g, Nb * H * W))
+        else:
+            assert cs.stride == 2
+            zero_needed = False
+            for r in (0, 1):
+                for c in (0, 1):
+                    kh0, kw0 = (r + cs.pad) % 2, (c + cs.pad) % 2
+                    nkh = (KH - kh0 + 1) // 2 if kh0 < KH else 0
+                    nkw = (KW - kw0 + 1) // 2 if kw0 < KW else 0
+                    ohc, owc = (H - r + 1) // 2, (W - c + 1) // 2
+                    if ohc == 0 or owc == 0:
+                        continue
+                    if nkh == 0 or nkw == 0:
+                        zero_needed = True
+                        continue
+                    wt = torch.empty((Ci, nkh, nkw, Co), device=dev, dtype=torch.bfloat16)
+                    ops.weight_transform(w, wt, [Co, KH, KW, Ci, nkh, nkw, kh0, 2, kw0, 2])
+                    ih0 = (r + cs.pad - kh0) // 2
+                    iw0 = (c + cs.pad - kw0) // 2
+                    g = [Nb, OH, OW, Co, ohc, owc, nkh, nkw, 1, 1, -1, -1, ih0, iw0, Ci,
+                         H, W, 2, 2, r, c, Ci]
+                    launches.append((wt, g, Nb * ohc * owc))
+            if zero_needed:
+                assert bn_epi is None, "BN-epilogue dgrad needs every output position covered"
+                if not accumulate:
+                    dx.zero_()
+        if bn_epi is None:
+            epi = (1, dx, None) if accumulate else None
+            for wt, g, M in launches:
+                v = igemm_choose(ops, dyn, wt, dx, g, epi=epi)
+                igemm_launch(ops, dyn, wt, dx, g, v, epi=epi)
+            return dx, None, 0
+        assert not accumulate
+        if bn_epi[0] == "mask":
+            _, a_prev, bs = bn_epi
+            epi = (3, None, a_prev)
+            tables = (bs.ss.view(-1), bs.mi)
+        else:
+            _, resid, y, a_prev, mi = bn_epi
+            epi = (4, resid, y, a_prev)
+            tables = (None, mi)
+        chosen = []
+        for wt, g, M in launches:
+            seg = M // S
+            v = igemm_choose(ops, dyn, wt, dx, g, want_stats=True, epi=epi, seg_rows=seg,
+                             epi_tables=tables)
+            chosen.append((wt, g, M, seg, ops.igemm_variant_bm(v), v))
+        seg_blocks = sum(seg // bm for (_, _, _, seg, bm, _) in chosen)
+        partial = torch.empty((S * seg_blocks * 2 * Ci,), device=dev, dtype=torch.float32)
+        base = 0
+        for wt, g, M, seg, bm, v in chosen:
+            igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
+                         epi_tables=tables, remap=(seg_blocks, base))
+            base += seg // bm
+        return dx, partial, seg_blocks
+
+    # ------------------------------------------------------------------ forward / backward
+    def forward(self, xn: torch.Tensor) -> Tuple[torch.Tensor, List[_BlockTape]]:
+        ops = _ext.ops()
+        st = pstate.get()
+        S = self.S
+        self.calls += 1
+        tapes: List[_BlockTape] = []
+        x = xn
+        for b in self.blocks:
+            tp = _BlockTape(x=x)
+            pro_ss = None
+            cur = x
+            for cs in b.convs:
+                if pro_ss is not None and cs.k > 1:
+                    # a k x k conv re-gathers every input pixel k² times: applying BN+ReLU in
+                    # its prologue costs more VALU work than one materialising pass (measured)
+                    bmat = torch.empty_like(cur)
+                    ops.bn_apply_ss(cur, pro_ss, None, None, bmat, S, True)
+                    cur, pro_ss = bmat, None
+                tp.ins.append((cur, pro_ss))
+                a, partial, nblk = self._conv_fwd(ops, cur, cs, pro_ss, S)
+                rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
+                bs = self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st)
+                tp.acts.append(a)
+                tp.bns.append(bs)
+                cur, pro_ss = a, bs.ss
+            aL, bsL = tp.acts[-1], tp.bns[-1]
+            out = torch.empty_like(aL)
+            if b.down is not None:
+                ad, partial, nblk = self._conv_fwd(ops, x, b.down, None, S)
+                rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
+                tp.ad = ad
+                tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st)
+                ops.bn_apply_ss(aL, bsL.ss, ad, tp.bnd.ss, out, S, True)
+            else:
+                ops.bn_apply_ss(aL, bsL.ss, x, None, out, S, True)
+            tp.out = out
+            tapes.append(tp)
+            x = out
+        return x, tapes
+
+    def backward(self, gout: torch.Tensor, tapes: List[_BlockTape]) -> torch.Tensor:
+        ops = _ext.ops()
+        st = pstate.get()
+        S = self.S
+        g, pre = gout, None
+        for idx in range(len(self.blocks) - 1, -1, -1):
+            prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else None
+            g, pre = self._block_backward(ops, st, S, self.blocks[idx], tapes[idx], g, pre, prev)
+        return g
+
+    def _block_backward(self, ops, st, S, b: _BlockSpec, tp: _BlockTape, g: torch.Tensor,
+                        pre: Optional[Tuple[torch.Tensor, int]], prev):
+        """``g`` = dL/d(block output).  ``pre = None``: g is the raw gradient; otherwise g is
+        already ReLU-masked and ``pre`` holds the last BN's Σg, Σg·x̂ partials (computed by the
+        following block's dgrad epilogue).  Returns the same pair for the block input: masked +
+        partials when the producer is another block of this executor (``prev``), raw
+        otherwise."""
+        out = tp.out
+        L = len(b.convs) - 1
+        aL, bsL = tp.acts[L], tp.bns[L]
+        C = aL.shape[-1]
+        R = aL.numel() // C
+        dev = aL.device
+        da = torch.empty_like(aL)
+        if pre is None:
+            nblk = ops.bn_blocks(R, C, S)
+            partial = torch.empty((S * nblk * 2 * C,), device=dev, dtype=torch.float32)
+            ops.bn_bwd_reduce(g, out, aL, bsL.mi, S, True, partial)
+            coefL = self._bn_bwd(ops, b.convs[L].bn, partial, nblk, bsL, S, st)
+            g3 = torch.empty_like(out)
+            ops.bn_bwd_apply(g, out, aL, coefL, S, True, da, g3)  # g3 = g·[out > 0]
+        else:
+            partial, nblk = pre
+            g3 = g
+            coefL = self._bn_bwd(ops, b.convs[L].bn, partial, nblk, bsL, S, st)
+            ops.bn_bwd_apply(g3, None, aL, coefL, S, False, da, None)
+        dad = None
+        if b.down is not None:
+            nblk_d = ops.bn_blocks(R, C, S)
+            partial_d = torch.empty((S * nblk_d * 2 * C,), device=dev, dtype=torch.float32)
+            ops.bn_bwd_reduce(g3, None, tp.ad, tp.bnd.mi, S, False, partial_d)
+            coefd = self._bn_bwd(ops, b.down.bn, partial_d, nblk_d, tp.bnd, S, st)
+            dad = torch.empty_like(tp.ad)
+            ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
+        # conv chain, last to first
+        for i in range(L, 0, -1):
+            cs = b.convs[i]
+            xin, pro_ss = tp.ins[i]
+            self._wgrad(ops, da, xin, cs, pro_ss, S)
+            a_prev, bs_prev = tp.acts[i - 1], tp.bns[i - 1]
+            gm, part, nb = self._dgrad(ops, da, cs, a_prev.shape, S, bn_epi=("mask", a_prev, bs_prev))
+            coef = self._bn_bwd(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
+            da = torch.empty_like(a_prev)
+            ops.bn_bwd_apply(gm, None, a_prev, coef, S, False, da, None)
+        cs0 = b.convs[0]
+        self._wgrad(ops, da, tp.x, cs0, None, S)
+        if b.down is not None:
+            self._wgrad(ops, dad, tp.x, b.down, None, S)
+            resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
+        else:
+            resid = g3
+        if prev is None:
+            dx, _, _ = self._dgrad(ops, da, cs0, tp.x.shape, S, accumulate=True, dx=resid)
+            return dx, None
+        pb, ptp = prev
+        dx = resid if b.down is not None else None
+        gx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S, dx=dx,
+                                   bn_epi=("res", resid, tp.x, ptp.acts[-1], ptp.bns[-1].mi))
+        return gx, (part, nb)
+
+
+class FusedStagesFn(torch.autograd.Function):
+    """Autograd boundary around the executor: input = stem output (channels_last bf16),
+    output = last block output; parameter gradients bypass autograd (flat store)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, ex: FusedStages):
+        xn = x.permute(0, 2, 3, 1)
+        if not xn.is_contiguous():
+            xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+        out, tapes = ex.forward(xn)
+        ctx.ex = ex
+        ctx.tapes = tapes
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gout):
+        if gout.dtype != torch.bfloat16:
+            gout = gout.to(torch.bfloat16)
+        gn = gout.permute(0, 2, 3, 1)
+        if not gn.is_contiguous():
+            gn = gout.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+        dx = ctx.ex.backward(gn, ctx.tapes)
+        ctx.tapes = None
+        return dx.permute(0, 3, 1, 2), None, None

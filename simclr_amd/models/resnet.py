@@ -29,6 +29,7 @@ MI355X-first differences from the reference:
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, List, Optional, Type
 
 import torch
@@ -154,12 +155,35 @@ class ResNet(nn.Module):
             layers.append(block(self.inplanes, planes))
         return nn.Sequential(*layers)
 
+    # the fused stage executor (models/fused.py) runs layer1..layer4 in training on the HIP
+    # path; ``use_fused_stages = False`` (or SIMCLR_FUSED=0) keeps the per-module path
+    use_fused_stages = os.environ.get("SIMCLR_FUSED", "1") != "0"
+
+    def _fused_executor(self, x: torch.Tensor, segments: int):
+        if not (self.training and self.use_fused_stages and torch.is_grad_enabled()
+                and x.is_cuda and x.dtype == torch.bfloat16):
+            return None
+        from ..ops import registry
+        if not registry.use_hip(x):
+            return None
+        from .fused import FusedStages
+        cache = self.__dict__.setdefault("_fused_cache", {})
+        ex = cache.get(segments)
+        if ex is None:
+            ex = cache[segments] = FusedStages(self, segments)
+        return ex if ex.supported(x) else None
+
     def forward_features(self, x: torch.Tensor, segments: int = 1) -> torch.Tensor:
         x = self.bn1(self.conv1(x), relu=True, segments=segments)
         x = self.maxpool(x)
-        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
-            for blk in layer:
-                x = blk(x, segments=segments)
+        ex = self._fused_executor(x, segments)
+        if ex is not None:
+            from .fused import FusedStagesFn
+            x = FusedStagesFn.apply(x, self.layer1[0].conv1.weight, ex)
+        else:
+            for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+                for blk in layer:
+                    x = blk(x, segments=segments)
         return global_avg_pool(x)
 
     def forward(self, x: torch.Tensor, segments: int = 1) -> torch.Tensor:

@@ -24,6 +24,55 @@ import torch
 from . import _ext, tuning
 
 
+def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None,
+                 seg_rows: int = 0, epi_tables=None) -> int:
+    """Autotuned tile variant for this problem (admissible: BM divides the segment rows /
+    M whenever per-segment prologue, statistics or the mode-3 epilogue need block-uniform
+    segments)."""
+    M = geom[0] * geom[4] * geom[5]
+    N = geom[14]
+    psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
+    emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
+    ess, emi = epi_tables if epi_tables is not None else (None, None)
+    cands = []
+    for v in range(ops.igemm_nvariants()):
+        bm = ops.igemm_variant_bm(v)
+        if want_stats and M % bm:
+            continue
+        if psc is not None and pseg % bm:
+            continue
+        if seg_rows and seg_rows % bm:
+            continue
+        cands.append(v)
+    if not cands:
+        raise ValueError(f"no igemm tile variant admissible for M={M} segment rows "
+                         f"{seg_rows or pseg}")
+    default = 1 if N <= 64 else 0
+    if default not in cands:
+        default = cands[0]
+    key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows)
+    ec = epi[3] if epi is not None and len(epi) > 3 else None
+
+    def trial(v):
+        bm = ops.igemm_variant_bm(v)
+        st = (torch.empty(((M + bm - 1) // bm) * 2 * N, device=out.device, dtype=torch.float32)
+              if want_stats else None)
+        ops.igemm(A, B, torch.empty_like(out), bias, st, geom, psc, psh, pseg, prelu, emode, ea,
+                  eb, v, ess, emi, seg_rows, 0, 0, ec)
+
+    return tuning.pick(key, cands, default, trial)
+
+
+def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
+                 seg_rows: int = 0, epi_tables=None, remap=(0, 0)) -> None:
+    psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
+    emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
+    ec = epi[3] if epi is not None and len(epi) > 3 else None
+    ess, emi = epi_tables if epi_tables is not None else (None, None)
+    ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
+              seg_rows, remap[0], remap[1], ec)
+
+
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):
     """Launch the implicit GEMM with the autotuned tile variant for this problem.
 
@@ -31,41 +80,18 @@ def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=N
     A operand; epi = (mode, a, b) accumulates into the output.  Returns (stats, nblk) or None."""
     M = geom[0] * geom[4] * geom[5]
     N = geom[14]
-    psc, psh, seg_rows, prelu = pro if pro is not None else (None, None, 0, False)
-    emode, ea, eb = epi if epi is not None else (0, None, None)
-    cands = []
-    for v in range(ops.igemm_nvariants()):
-        bm = ops.igemm_variant_bm(v)
-        if want_stats and M % bm:
-            continue
-        if psc is not None and seg_rows % bm:
-            continue
-        cands.append(v)
-    default = 1 if N <= 64 else 0
-    if not cands:
-        if psc is not None:
+    try:
+        v = igemm_choose(ops, A, B, out, geom, bias, want_stats, pro, epi)
+    except ValueError:
+        if pro is not None:
             raise ValueError("BN prologue fusion impossible for this shape")
         want_stats = False
-        cands = list(range(ops.igemm_nvariants()))
-    if default not in cands:
-        default = cands[0]
-    key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None)
-
-    def launch(v, o, st):
-        ops.igemm(A, B, o, bias, st, geom, psc, psh, seg_rows, prelu, emode, ea, eb, v)
-
-    def trial(v):
-        bm = ops.igemm_variant_bm(v)
-        st = (torch.empty(((M + bm - 1) // bm) * 2 * N, device=out.device, dtype=torch.float32)
-              if want_stats else None)
-        launch(v, torch.empty_like(out), st)
-
-    v = tuning.pick(key, cands, default, trial)
+        v = igemm_choose(ops, A, B, out, geom, bias, False, pro, epi)
     bm = ops.igemm_variant_bm(v)
     stats = None
     if want_stats:
         stats = torch.empty(((M // bm) * 2 * N,), device=out.device, dtype=torch.float32)
-    launch(v, out, stats)
+    igemm_launch(ops, A, B, out, geom, v, bias, stats, pro, epi)
     return (stats, M // bm) if stats is not None else None
 
 

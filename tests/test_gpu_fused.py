@@ -1,0 +1,171 @@
+"""Fused ResNet-stage executor (``simclr_amd/models/fused.py``) and the kernel features it uses:
+the mode-3 dgrad epilogue (ReLU mask + BatchNorm-backward partials, segment-major stats remap
+across the stride-2 parity classes), ``bn_apply_ss`` and the finalize scale/shift table — each
+against a plain PyTorch fp32 reference — and the whole executor against the per-module path."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from simclr_amd.ops import _ext
+    _ext.require()
+    return torch.ops.simclr_amd
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return (a.float() - b.float()).abs().max().item() / (b.float().abs().max().item() + 1e-6)
+
+
+@pytest.mark.parametrize("k,s,p", [(1, 1, 0), (3, 1, 1), (3, 2, 1)])
+def test_dgrad_mode3_epilogue(ops, k, s, p):
+    from simclr_amd.models.fused import FusedStages, _BNState, _ConvSpec
+    torch.manual_seed(3)
+    N, Ci, H, W, Co, S = 8, 64, 16, 16, 128, 2
+    conv = torch.nn.Conv2d(Ci, Co, k, s, p, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(_bf(torch.randn_like(conv.weight) / math.sqrt(Ci * k * k)).float())
+    OH = (H + 2 * p - k) // s + 1
+    dy = _bf(torch.randn(N, OH, OH, Co, device=DEV))
+    a_prev = _bf(torch.randn(N, H, W, Ci, device=DEV))
+    sc = torch.rand(S, Ci, device=DEV) + 0.5
+    sh = torch.randn(S, Ci, device=DEV) * 0.3
+    mean = torch.randn(S, Ci, device=DEV) * 0.2
+    inv = torch.rand(S, Ci, device=DEV) + 0.5
+    bs = _BNState(torch.cat([mean, inv]).reshape(-1).contiguous(),
+                  torch.stack([sc, sh]).reshape(2, S * Ci).contiguous(), 1.0)
+    ex = FusedStages.__new__(FusedStages)
+    cs = _ConvSpec(conv, None, s, k, p)
+    gm, part, nb = ex._dgrad(ops, dy, cs, a_prev.shape, S, bn_epi=("mask", a_prev, bs))
+    sums = torch.empty(2 * S * Ci, device=DEV)
+    ops.bn_reduce(part, nb, S, Ci, sums)
+    # fp32 reference
+    dx = torch.nn.grad.conv2d_input((N, Ci, H, W), conv.weight.float(),
+                                    dy.permute(0, 3, 1, 2).float(), s, p)
+    dx = _bf(dx).float().permute(0, 2, 3, 1)
+    seg = (torch.arange(N, device=DEV) // (N // S))[:, None, None, None]
+    af = a_prev.float()
+    mask = af * sc[seg.squeeze()][:, None, None, :] + sh[seg.squeeze()][:, None, None, :] > 0
+    g = torch.where(mask, dx, 0.0)
+    assert _rel(gm, g) < 2e-2
+    xh = (af - mean[seg.squeeze()][:, None, None, :]) * inv[seg.squeeze()][:, None, None, :]
+    gk = gm.float()  # the kernel's (bf16) g drives its own sums: compare against them
+    ref1 = gk.reshape(S, -1, Ci).sum(1)
+    ref2 = (gk * xh).reshape(S, -1, Ci).sum(1)
+    got = sums.view(2, S, Ci)
+    assert _rel(got[0], ref1) < 1e-3
+    assert _rel(got[1], ref2) < 1e-3
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_bn_apply_ss_and_finalize_table(ops, mode):
+    torch.manual_seed(1)
+    S, R, C = 2, 4096, 256
+    x = _bf(torch.randn(S * R, C, device=DEV))
+    res = _bf(torch.randn(S * R, C, device=DEV))
+    stats = torch.stack([x.float().view(S, R, C).sum(1), (x.float() ** 2).view(S, R, C).sum(1)])
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV)
+    mi = torch.empty(2 * S * C, device=DEV)
+    ss = torch.empty(2 * S * C, device=DEV)
+    ops.bn_finalize(stats.reshape(-1).contiguous(), S, C, float(R), 1e-5, 0.1, None, None, mi,
+                    None, gamma, beta, ss)
+    mean = stats[0] / R
+    var = stats[1] / R - mean ** 2
+    scale = gamma * torch.rsqrt(var + 1e-5)
+    shift = beta - mean * scale
+    assert torch.allclose(ss.view(2, S, C)[0], scale, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(ss.view(2, S, C)[1], shift, rtol=1e-4, atol=1e-4)
+    y = torch.empty_like(x)
+    rss = torch.stack([torch.rand(S, C, device=DEV), torch.randn(S, C, device=DEV)]).contiguous()
+    ref = x.float().view(S, R, C) * scale[:, None] + shift[:, None]
+    if mode == 0:
+        ops.bn_apply_ss(x, ss, None, None, y, S, True)
+    elif mode == 1:
+        ops.bn_apply_ss(x, ss, res, None, y, S, True)
+        ref = ref + res.float().view(S, R, C)
+    else:
+        ops.bn_apply_ss(x, ss, res, rss.view(-1), y, S, True)
+        ref = ref + res.float().view(S, R, C) * rss[0][:, None] + rss[1][:, None]
+    ref = torch.relu(ref).reshape(S * R, C)
+    assert _rel(y, ref) < 1e-2
+
+
+def _model(base, stem, device, shadow=torch.bfloat16):
+    from simclr_amd.models.contrastive import ContrastiveModel
+    from simclr_amd.parallel import state as pstate
+    from simclr_amd.parallel.flat import FlatParamStore
+    pstate.reset()
+    pstate.get().device = device
+    torch.manual_seed(0)
+    m = ContrastiveModel(base_cnn=base, d=128, cifar_stem=stem).to(device)
+    store = FlatParamStore(m, device, shadow_dtype=shadow)
+    m.train()
+    return m, store
+
+
+@pytest.mark.parametrize("base,stem,batch", [("resnet50", True, 32), ("resnet18", None, 64),
+                                             ("resnet50", True, 64)])
+def test_fused_stages_match_module_path(base, stem, batch):
+    """Same weights / input: the executor is at least as close to the fp32 torch reference as
+    the per-module bf16 path — loss, every parameter gradient (flat buffer) and every running
+    statistic.  (At random init the NT-Xent gradient is a small difference of nearly equal
+    embeddings, so bf16 rounding alone moves some gradients by tens of percent: the check is
+    relative to the module path's own distance from fp32, not an absolute tolerance.)"""
+    from simclr_amd.loss.ntxent import NTXent
+    dev = torch.device(DEV, 0)
+    torch.manual_seed(5)
+    x = _bf(torch.rand(2 * batch, 8, 32, 32, device=dev)).contiguous(
+        memory_format=torch.channels_last)
+    res = {}
+    for mode in ("module", "fused", "fp32"):
+        m2, store2 = _model(base, stem, dev)
+        m2.f.use_fused_stages = mode == "fused"
+        if mode == "fp32":
+            with torch.no_grad():  # same (bf16-representable) weights, fp32 compute
+                store2.master.copy_(store2.shadow.float())
+            store2.shadow = None
+            for sl in store2.slots:
+                sl.shadow = None
+        store2.zero_grad()
+        xin = x.float()[:, :3].contiguous() if mode == "fp32" else x
+        z = m2(xin, segments=2)
+        loss = NTXent(temperature=0.5)(z)
+        loss.backward()
+        torch.cuda.synchronize()
+        if mode == "fused":
+            ex = m2.f.__dict__.get("_fused_cache", {}).get(2)
+            assert ex is not None and ex.calls == 1, "fused executor did not run"
+        res[mode] = (float(loss.detach()), store2.grad.clone(),
+                     [(n, b.float().clone()) for n, b in m2.named_buffers() if "running" in n])
+    lm, gm, bm = res["module"]
+    lf, gf, bf = res["fused"]
+    lr, gr, br = res["fp32"]
+    assert abs(lf - lr) <= 1.5 * abs(lm - lr) + 5e-3, (lm, lf, lr)
+    for (name, u), (_, v), (_, w) in zip(bf, bm, br):
+        ef = (u - w).norm().item() / (w.norm().item() + 1e-6)
+        em = (v - w).norm().item() / (w.norm().item() + 1e-6)
+        assert ef <= 1.5 * em + 1e-2, (name, ef, em)
+    _, store = _model(base, stem, dev)
+    tot_f = (gf - gr).norm().item() / gr.norm().item()
+    tot_m = (gm - gr).norm().item() / gr.norm().item()
+    assert tot_f <= 1.5 * tot_m + 1e-2, (tot_f, tot_m)
+    for (o, n_), name in zip(store.segments(), store.names):
+        w = gr[o:o + n_]
+        denom = w.norm().item()
+        if denom < 1e-8:
+            continue
+        ef = (gf[o:o + n_] - w).norm().item() / denom
+        em = (gm[o:o + n_] - w).norm().item() / denom
+        assert ef <= 1.5 * em + 0.05, (name, ef, em)

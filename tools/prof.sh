@@ -1,7 +1,7 @@
 #!/bin/bash
 # Usage (on the GPU box, from the repo root): tools/prof.sh NAME -- python3 script.py args...
-# Runs rocprofv3 kernel-trace+stats (CSV) and keeps only the small summary files under
-# gpurun_out/prof_NAME (the per-dispatch trace is deleted to stay under gpurun's copy-back cap).
+# Runs rocprofv3 kernel-trace+stats (CSV) under gpurun_out/prof_NAME, writes a per-step summary
+# (tools/trace_summary.py) next to it and drops the per-dispatch trace if it is large.
 set -o pipefail
 name=$1; shift; [ "$1" == "--" ] && shift
 root=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -11,6 +11,10 @@ export TMPDIR=/tmp
 cd /tmp
 rocprofv3 --kernel-trace --stats -f csv -T -d "$out" -o run -- "$@"
 rc=$?
-find "$out" -name '*kernel_trace.csv' -size +2M -delete
+if [ -f "$out/run_kernel_trace.csv" ]; then
+  python3 "$root/tools/trace_summary.py" "$out/run_kernel_trace.csv" --steps ${PROF_STEPS:-5} --list \
+    > "$out/summary.md" 2>&1 || true
+fi
+find "$out" -name '*kernel_trace.csv' -size +20M -delete
 find "$out" -name '*.db' -delete
 exit $rc
