@@ -4,6 +4,7 @@
 // hand-written kernel: an out-of-bounds access can take the whole node down).
 #include <ATen/core/Tensor.h>
 #include <ATen/ops/empty.h>
+#include <ATen/ops/zeros.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/util/Exception.h>
 #include <torch/library.h>
@@ -260,6 +261,71 @@ void bn_final(const Tensor& stats, int64_t S, int64_t C, double count, double ep
               optf32(gamma, "gamma"), optf32(beta, "beta"), optf32w(ss, "ss"), cur_stream());
 }
 
+// persistent zeroed ticket array for the last-arriver reductions (per device)
+unsigned* tickets_for(const Tensor& like, int64_t n) {
+  static std::vector<Tensor> per_dev;
+  const int d = like.get_device();
+  if ((int)per_dev.size() <= d) per_dev.resize(d + 1);
+  if (!per_dev[d].defined() || per_dev[d].numel() < n) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(cur_stream(), &cs);
+    TORCH_CHECK(cs == hipStreamCaptureStatusNone,
+                "bn ticket array must be allocated before graph capture");
+    per_dev[d] = at::zeros({std::max<int64_t>(n, 4096)}, like.options().dtype(at::kInt));
+  }
+  return reinterpret_cast<unsigned*>(per_dev[d].data_ptr<int>());
+}
+
+void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t C, int64_t mode,
+                        const c10::optional<Tensor>& stats, double count, double eps,
+                        double momentum, const c10::optional<Tensor>& rm,
+                        const c10::optional<Tensor>& rv, const c10::optional<Tensor>& mi,
+                        const c10::optional<Tensor>& nbt, const c10::optional<Tensor>& gamma,
+                        const c10::optional<Tensor>& beta, const c10::optional<Tensor>& ss,
+                        const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta,
+                        const c10::optional<Tensor>& coef) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "bn_reduce_fused: mode");
+  TORCH_CHECK(nblk > 0 && partial.numel() >= S * nblk * 2 * C, "bn_reduce_fused: partial size");
+  BnReduceFusedParams q;
+  q.partial = f32(partial, "partial");
+  q.nblk = (int)nblk; q.S = (int)S; q.C = (int)C; q.mode = (int)mode;
+  const int G = bn_reduce_groups((int)nblk);
+  at::Tensor ws = at::empty({S * G * 2 * C}, partial.options());
+  q.ws = ws.data_ptr<float>();
+  q.tickets = tickets_for(partial, (C + 63) / 64);
+  q.count = (float)count; q.eps = (float)eps; q.momentum = (float)momentum;
+  if (mode == 0) {
+    TORCH_CHECK(stats.has_value() && stats->numel() >= 2 * S * C, "bn_reduce_fused: stats");
+    q.stats = f32w(*stats, "stats");
+  } else if (mode == 1) {
+    TORCH_CHECK(mi.has_value() && mi->numel() >= 2 * S * C, "bn_reduce_fused: mi");
+    q.mi = f32w(*mi, "mi");
+    q.running_mean = optf32w(rm, "running_mean");
+    q.running_var = optf32w(rv, "running_var");
+    if (nbt.has_value() && nbt->defined()) {
+      check_dev(*nbt, at::kLong, "num_batches_tracked");
+      q.nbt = nbt->data_ptr<int64_t>();
+    }
+    q.gamma = optf32(gamma, "gamma");
+    q.beta = optf32(beta, "beta");
+    if (ss.has_value() && ss->defined()) TORCH_CHECK(ss->numel() >= 2 * S * C, "bn_reduce_fused: ss");
+    q.ss = optf32w(ss, "ss");
+  } else {
+    TORCH_CHECK(mi.has_value() && mi->numel() >= 2 * S * C, "bn_reduce_fused: mi");
+    TORCH_CHECK(coef.has_value() && coef->numel() >= 3 * S * C, "bn_reduce_fused: coef");
+    q.mi = const_cast<float*>(f32(*mi, "mi"));
+    q.gamma = optf32(gamma, "gamma");
+    q.dgamma = optf32w(dgamma, "dgamma");
+    q.dbeta = optf32w(dbeta, "dbeta");
+    q.coef = f32w(*coef, "coef");
+  }
+  if (q.gamma) TORCH_CHECK(gamma->numel() == C, "bn_reduce_fused: gamma size");
+  if (q.beta) TORCH_CHECK(beta->numel() == C, "bn_reduce_fused: beta size");
+  if (q.dgamma) TORCH_CHECK(dgamma->numel() == C, "bn_reduce_fused: dgamma size");
+  if (q.dbeta) TORCH_CHECK(dbeta->numel() == C, "bn_reduce_fused: dbeta size");
+  bn_reduce_fused(q, cur_stream());
+}
+
 void bn_apply_ss_op(const Tensor& x, const Tensor& ss, const c10::optional<Tensor>& res,
                     const c10::optional<Tensor>& rss, const Tensor& y, int64_t S, bool relu) {
   check_rc(x, S, "bn_apply_ss");
@@ -483,6 +549,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
   m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
+  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None) -> ()", &bn_reduce_fused_op);
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);

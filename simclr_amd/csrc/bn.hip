@@ -125,6 +125,154 @@ __global__ void k_reduce_partials(const float* __restrict__ partial, int nblk, i
   stats[(size_t)S * C + s * C + c] = b;
 }
 
+// ---------------------------------------------------------------------------------------------
+// One-launch BatchNorm reduction: partial [S][nblk][2][C] -> (per mode)
+//   mode 0: stats [2][S][C]                    (the cross-rank all-reduce input)
+//   mode 1: forward finalize (mean/invstd, scale/shift, running stats, num_batches_tracked)
+//   mode 2: backward finalize (dγ, dβ, coef [3][S][C])
+// Grid (ceil(C/64), S, G): every block sums a G-th of one segment's partial rows for 64
+// channels into ws [S][G][2][C]; the last of the S·G blocks of a channel group to arrive (agent-
+// scope release/acquire around a per-group ticket, cdna_hip_programming.md §5 item 2) sums the
+// G slices in fixed order and finalizes: deterministic, and three launches become one.
+// Tickets live in a persistent zeroed array; the last arriver resets its own ticket, so the op
+// must stay on one stream (it does: the compute stream).
+struct BnReduceArgs {
+  const float* partial;
+  int nblk, S, C, G, mode;
+  float* ws;
+  unsigned* tickets;
+  float* stats;  // mode 0 out
+  // mode 1
+  float count, eps, momentum;
+  float* running_mean;
+  float* running_var;
+  float* mi;  // mode 1 out / mode 2 in
+  int64_t* nbt;
+  const float* gamma;
+  const float* beta;
+  float* ss;
+  // mode 2
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+};
+
+__global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
+  __shared__ float red[4][64][2];
+  __shared__ int last;
+  const int cl = threadIdx.x & 63;
+  const int lane = threadIdx.x >> 6;
+  const int cg = blockIdx.x;
+  const int c = cg * 64 + cl;
+  const int s = blockIdx.y, gz = blockIdx.z;
+  const int C = p.C, S = p.S, G = p.G;
+  const int per = (p.nblk + G - 1) / G;
+  const int beg = gz * per;
+  const int end = min(p.nblk, beg + per);
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    const float* src = p.partial + (size_t)s * p.nblk * 2 * C;
+#pragma unroll 4
+    for (int i = beg + lane; i < end; i += 4) {
+      a += src[(size_t)i * 2 * C + c];
+      b += src[(size_t)i * 2 * C + C + c];
+    }
+  }
+  red[lane][cl][0] = a;
+  red[lane][cl][1] = b;
+  __syncthreads();
+  // ---- publish this slice write-through (sc1: agent-scope relaxed atomic stores), so no
+  // release fence is needed — an agent release would write back this XCD's whole dirty L2,
+  // which right after a conv epilogue is megabytes (guide §6 Guideline 16, R1)
+  if (lane == 0 && c < C) {
+    a = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    b = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+    float* dst = p.ws + (((size_t)s * G + gz) * 2) * C;
+    __hip_atomic_store(dst + c, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + C + c, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old =
+        __hip_atomic_fetch_add(&p.tickets[cg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == (unsigned)(S * G - 1);
+    if (last)  // reset for the next launch (stream-ordered)
+      __hip_atomic_store(&p.tickets[cg], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  // consumer: ONE agent acquire (drops this CU's stale L1 lines), then plain, pipelined loads,
+  // the G slices of each segment split over the 4 waves and combined through LDS (fixed order)
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (p.mode == 1 && c == 0 && lane == 0 && p.nbt != nullptr) p.nbt[0] += S;  // one per view
+  float rm = 0.f, rv = 0.f, dg = 0.f, db = 0.f, gm = 1.f;
+  if (c < C) {
+    if (p.mode == 1) {
+      rm = p.running_mean ? p.running_mean[c] : 0.f;
+      rv = p.running_var ? p.running_var[c] : 0.f;
+    }
+    if (p.mode == 2) gm = p.gamma ? p.gamma[c] : 1.f;
+  }
+  const float unbias = p.count > 1.f ? p.count / (p.count - 1.f) : 1.f;
+  for (int sg = 0; sg < S; ++sg) {
+    float s1 = 0.f, s2 = 0.f;
+    if (c < C) {
+      for (int g = lane; g < G; g += 4) {
+        const float* src = p.ws + (((size_t)sg * G + g) * 2) * C;
+        s1 += src[c];
+        s2 += src[C + c];
+      }
+    }
+    __syncthreads();
+    red[lane][cl][0] = s1;
+    red[lane][cl][1] = s2;
+    __syncthreads();
+    if (lane != 0 || c >= C) continue;
+    s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+    if (p.mode == 0) {
+      p.stats[sg * C + c] = s1;
+      p.stats[S * C + sg * C + c] = s2;
+    } else if (p.mode == 1) {
+      const float mean = s1 / p.count;
+      float var = s2 / p.count - mean * mean;
+      var = var > 0.f ? var : 0.f;
+      const float inv = rsqrtf(var + p.eps);
+      p.mi[sg * C + c] = mean;
+      p.mi[S * C + sg * C + c] = inv;
+      if (p.ss != nullptr) {
+        const float sc = (p.gamma ? p.gamma[c] : 1.f) * inv;
+        p.ss[sg * C + c] = sc;
+        p.ss[S * C + sg * C + c] = (p.beta ? p.beta[c] : 0.f) - mean * sc;
+      }
+      rm = (1.f - p.momentum) * rm + p.momentum * mean;
+      rv = (1.f - p.momentum) * rv + p.momentum * var * unbias;
+    } else {
+      db += s1;
+      dg += s2;
+      const float mean = p.mi[sg * C + c], inv = p.mi[S * C + sg * C + c];
+      const float A = gm * inv;
+      const float bb = s1 / p.count, c2 = s2 / p.count;
+      p.coef[sg * C + c] = A;
+      p.coef[S * C + sg * C + c] = -A * c2 * inv;
+      p.coef[2 * S * C + sg * C + c] = -A * bb + A * c2 * inv * mean;
+    }
+  }
+  if (lane != 0 || c >= C) return;
+  if (p.mode == 1) {
+    if (p.running_mean) p.running_mean[c] = rm;
+    if (p.running_var) p.running_var[c] = rv;
+  } else if (p.mode == 2) {
+    if (p.dgamma) p.dgamma[c] = dg;
+    if (p.dbeta) p.dbeta[c] = db;
+  }
+}
+
 // stats [2][S][C] -> mean_invstd [2][S][C]; sequential running-stat updates per segment
 // Optionally also the fused-apply table ss [2][S][C]: scale = γ·invstd, shift = β − mean·scale.
 __global__ void k_bn_finalize(const float* __restrict__ stats, int S, int C, float count, float eps,
@@ -581,6 +729,19 @@ void bn_finalize(const float* stats, int S, int C, float count, float eps, float
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, stats, S, C, count, eps,
                      momentum, running_mean, running_var, mean_invstd, nbt, gamma, beta,
                      scale_shift);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s) {
+  BnReduceArgs a{};
+  a.partial = q.partial; a.nblk = q.nblk; a.S = q.S; a.C = q.C; a.mode = q.mode;
+  a.G = bn_reduce_groups(q.nblk);
+  a.ws = q.ws; a.tickets = q.tickets; a.stats = q.stats;
+  a.count = q.count; a.eps = q.eps; a.momentum = q.momentum;
+  a.running_mean = q.running_mean; a.running_var = q.running_var; a.mi = q.mi; a.nbt = q.nbt;
+  a.gamma = q.gamma; a.beta = q.beta; a.ss = q.ss;
+  a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.coef = q.coef;
+  hipLaunchKernelGGL(k_bn_reduce_fused, dim3((q.C + 63) / 64, q.S, a.G), dim3(256), 0, s, a);
   HIP_CHECK_LAUNCH();
 }
 

@@ -537,9 +537,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
     }
 }
 
-// out[co][tap][ci < Creal] (+)= Σ_s partial[s][co][tap*C + ci]
+// out[co][tap][ci < Creal] (+)= Σ_s partial[s*stride][co][tap*C + ci]   (slab stride in slabs)
 __global__ void wgrad_reduce(const float* __restrict__ partial, float* __restrict__ out, int splits,
-                             int N, int K, int C, int Creal, float beta) {
+                             int sstride, int N, int K, int C, int Creal, float beta) {
   const int taps = K / C;
   const size_t total = (size_t)N * taps * Creal;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -550,18 +550,18 @@ __global__ void wgrad_reduce(const float* __restrict__ partial, float* __restric
     const int co = (int)(t / taps);
     const size_t src = (size_t)co * K + tap * C + ci;
     float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += partial[(size_t)sp * N * K + src];
+    for (int sp = 0; sp < splits; ++sp) s += partial[(size_t)sp * sstride * N * K + src];
     out[idx] = beta != 0.f ? beta * out[idx] + s : s;
   }
 }
 
 __global__ void wgrad_reduce_vec4(const float4* __restrict__ partial, float4* __restrict__ out,
-                                  int splits, size_t n4, float beta) {
+                                  int splits, int sstride, size_t n4, float beta) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
     float4 s = partial[i];
     for (int sp = 1; sp < splits; ++sp) {
-      const float4 v = partial[(size_t)sp * n4 + i];
+      const float4 v = partial[(size_t)sp * sstride * n4 + i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     if (beta != 0.f) {
@@ -569,6 +569,25 @@ __global__ void wgrad_reduce_vec4(const float4* __restrict__ partial, float4* __
       s.x += beta * o.x; s.y += beta * o.y; s.z += beta * o.z; s.w += beta * o.w;
     }
     out[i] = s;
+  }
+}
+
+// Level 1 of a many-split reduction: slab g*group (+)= slabs g*group+1 .. g*group+group-1, in
+// place (each float4 index is owned by one thread), so the final pass reads splits/group slabs.
+// A small weight (few output tiles) gets hundreds of M-splits: summing them serially per output
+// element was latency-bound (tens of µs for a 16K-float gradient).
+__global__ void wgrad_reduce_l1(float4* __restrict__ partial, int splits, int group, size_t n4) {
+  const int g = blockIdx.y;
+  const int s0 = g * group;
+  const int s1 = min(splits, s0 + group);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float4 s = partial[(size_t)s0 * n4 + i];
+    for (int sp = s0 + 1; sp < s1; ++sp) {
+      const float4 v = partial[(size_t)sp * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    partial[(size_t)s0 * n4 + i] = s;
   }
 }
 
@@ -726,18 +745,30 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     default: launch_wgrad<64, 64, 2, 2>(a, s); break;
   }
   const int K = a.K;
+  const size_t n4 = (size_t)a.N * K / 4;
+  int sstride = 1, count = splits;
+  constexpr int GROUP = 16;
+  if (splits > 2 * GROUP && (a.N * K) % 4 == 0) {
+    const int G = (splits + GROUP - 1) / GROUP;
+    int bx = (int)((n4 + 255) / 256);
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(wgrad_reduce_l1, dim3(bx, G), dim3(256), 0, s, (float4*)partial, splits,
+                       GROUP, n4);
+    HIP_CHECK_LAUNCH();
+    sstride = GROUP;
+    count = G;
+  }
   if (Creal == g.C) {
-    const size_t n4 = (size_t)a.N * K / 4;
     int blocks = (int)((n4 + 255) / 256);
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(wgrad_reduce_vec4, dim3(blocks), dim3(256), 0, s, (const float4*)partial,
-                       (float4*)out, splits, n4, beta);
+                       (float4*)out, count, sstride, n4, beta);
   } else {
     const size_t total = (size_t)a.N * (K / g.C) * Creal;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, out, splits, a.N, K,
-                       g.C, Creal, beta);
+    hipLaunchKernelGGL(wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, out, count, sstride,
+                       a.N, K, g.C, Creal, beta);
   }
   HIP_CHECK_LAUNCH();
 }

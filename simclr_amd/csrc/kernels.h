@@ -64,6 +64,27 @@ void bn_reduce_partials(const float* partial, int nblk_per_seg, int S, int C, fl
 void bn_finalize(const float* stats, int S, int C, float count, float eps, float momentum,
                  float* running_mean, float* running_var, float* mean_invstd, int64_t* nbt,
                  const float* gamma, const float* beta, float* scale_shift, hipStream_t s);
+// One-launch reduce of [S][nblk][2][C] partials + (mode 0) stats out, (1) forward finalize,
+// (2) backward finalize.  ws = S*groups*2*C floats; tickets = >= ceil(C/64) zeroed uints.
+struct BnReduceFusedParams {
+  const float* partial = nullptr;
+  int nblk = 0, S = 1, C = 0, mode = 0;
+  float* ws = nullptr;
+  unsigned* tickets = nullptr;
+  float* stats = nullptr;
+  float count = 1.f, eps = 1e-5f, momentum = 0.1f;
+  float* running_mean = nullptr;
+  float* running_var = nullptr;
+  float* mi = nullptr;
+  int64_t* nbt = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float* ss = nullptr;
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
+  float* coef = nullptr;
+};
+void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s);
 // y = relu?(x*sc + sh + [res | res*rsc + rsh]); ss / rss are [2][S][C] scale/shift tables
 void bn_apply_ss(const uint16_t* x, const float* ss, const uint16_t* res, const float* rss,
                  uint16_t* y, int R, int C, int S, int relu, hipStream_t s);

@@ -179,28 +179,40 @@ class FusedStages:
     def _bn_fwd(self, ops, bn, partial, nblk_seg: int, rows_seg: int, S: int, st) -> _BNState:
         C = bn.num_features
         dev = partial.device
-        stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_reduce(partial, nblk_seg, S, C, stats)
-        _allreduce(stats, st)
         count = float(rows_seg * st.world_size)
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ss = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean, bn.running_var,
-                        mi, bn.num_batches_tracked, bn.weight.detach(), bn.bias.detach(), ss)
+        if st.world_size == 1:  # one launch: reduce + finalize (last-arriver)
+            ops.bn_reduce_fused(partial, nblk_seg, S, C, 1, None, count, bn.eps, bn.momentum,
+                                bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
+                                bn.weight.detach(), bn.bias.detach(), ss)
+        else:
+            stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats)
+            _allreduce(stats, st)
+            ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean,
+                            bn.running_var, mi, bn.num_batches_tracked, bn.weight.detach(),
+                            bn.bias.detach(), ss)
         return _BNState(mi, ss.view(2, S * C), count)
 
     def _bn_bwd(self, ops, bn, partial, nblk_seg: int, bs: _BNState, S: int, st) -> torch.Tensor:
         """Finalize a BN backward from Σg, Σg·x̂ partials: dγ, dβ → flat grads; returns coef."""
         C = bn.num_features
         dev = partial.device
-        sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_reduce(partial, nblk_seg, S, C, sums)
-        _allreduce(sums, st)
         coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
-        res = {}
+        if st.world_size == 1:
+            def run(dg, db):  # one launch: reduce + backward finalize (last-arriver)
+                ops.bn_reduce_fused(partial, nblk_seg, S, C, 2, None, bs.count, 0.0, 0.0, None,
+                                    None, bs.mi, None, bn.weight.detach(), None, None, dg, db,
+                                    coef)
+        else:
+            sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, sums)
+            _allreduce(sums, st)
 
-        def run(dg, db):
-            ops.bn_bwd_finalize(sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db, coef)
+            def run(dg, db):
+                ops.bn_bwd_finalize(sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db,
+                                    coef)
 
         gslot = getattr(bn.weight, "_slot", None)
         bslot = getattr(bn.bias, "_slot", None)

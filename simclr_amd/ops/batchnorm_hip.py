@@ -53,21 +53,25 @@ class BatchNormHipFn(torch.autograd.Function):
         xr = _rows(x)
         R = xr.shape[0]
         dev = x.device
-        stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         pre = getattr(x, "_simclr_stats", None)
         if pre is not None and pre[1] % S == 0:
             partial, nblk_total = pre
-            ops.bn_reduce(partial, nblk_total // S, S, C, stats)
+            nblk = nblk_total // S
         else:
             nblk = ops.bn_blocks(R, C, S)
             partial = torch.empty((S * nblk * 2 * C,), device=dev, dtype=torch.float32)
             ops.bn_stats(xr, S, partial)
-            ops.bn_reduce(partial, nblk, S, C, stats)
-        _allreduce(stats, st)
         count = float((R // S) * st.world_size)
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean, bn.running_var,
-                        mi, bn.num_batches_tracked)
+        if st.world_size == 1:
+            ops.bn_reduce_fused(partial, nblk, S, C, 1, None, count, bn.eps, bn.momentum,
+                                bn.running_mean, bn.running_var, mi, bn.num_batches_tracked)
+        else:
+            stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+            ops.bn_reduce_fused(partial, nblk, S, C, 0, stats)
+            _allreduce(stats, st)
+            ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean,
+                            bn.running_var, mi, bn.num_batches_tracked)
         y = _empty_like_cl(x)
         res_r = _rows(residual) if residual is not None else None
         ops.bn_apply(xr, res_r, _rows(y), mi, weight.detach(), bias.detach(), S, relu)
@@ -92,13 +96,17 @@ class BatchNormHipFn(torch.autograd.Function):
         nblk = ops.bn_blocks(R, C, S)
         partial = torch.empty((S * nblk * 2 * C,), device=dev, dtype=torch.float32)
         ops.bn_bwd_reduce(dyr, yr, xr, mi, S, relu, partial)
-        sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_reduce(partial, nblk, S, C, sums)
-        _allreduce(sums, st)
         dgamma, gslot = _grad_out(weight)
         dbeta, bslot = _grad_out(ctx.bias)
         coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_bwd_finalize(sums, mi, weight.detach(), S, C, count, dgamma, dbeta, coef)
+        if st.world_size == 1:
+            ops.bn_reduce_fused(partial, nblk, S, C, 2, None, count, 0.0, 0.0, None, None, mi,
+                                None, weight.detach(), None, None, dgamma, dbeta, coef)
+        else:
+            sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+            ops.bn_reduce_fused(partial, nblk, S, C, 0, sums)
+            _allreduce(sums, st)
+            ops.bn_bwd_finalize(sums, mi, weight.detach(), S, C, count, dgamma, dbeta, coef)
         if gslot is not None:
             gslot.store.mark_ready(gslot.index)
         if bslot is not None:

@@ -11,6 +11,11 @@ import csv
 from collections import OrderedDict
 
 
+def _name(k: str, n: int) -> str:
+    k = k.replace("(anonymous namespace)::", "").replace("void ", "")
+    return k.split("(")[0][:n]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -28,7 +33,7 @@ def main():
     sel = rows[lo:hi]
     tot = OrderedDict()
     for r in sel:
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "")[:70]
+        name = _name(r["Kernel_Name"], 70)
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         c = tot.setdefault(name, [0, 0.0])
         c[0] += 1
@@ -43,7 +48,7 @@ def main():
         print("\n## last step, in order\n\n| # | kernel | grid | LDS | us |\n|---|---|---:|---:|---:|")
         last = rows[ends[-2] + 1:ends[-1] + 1]
         for i, r in enumerate(last):
-            name = r["Kernel_Name"].split("(")[0].replace("void ", "")[:60]
+            name = _name(r["Kernel_Name"], 60)
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             grid = r.get("Grid_Size_X", r.get("Grid_Size", "?"))
             lds = r.get("Group_Segment_Size", r.get("LDS_Block_Size", "?"))
