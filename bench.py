@@ -73,6 +73,7 @@ def run_ours(args, rank, world, dev):
         "LOCAL_RANK", "0")), group=dist.group.WORLD if world > 1 else None,
         backend=dist.get_backend() if world > 1 else "none")
     st.device = dev
+    pstate.make_stat_group(st)
     ov = [f"experiment.base_cnn={args.model}", f"experiment.batches={args.batch}",
           f"model.cifar_stem={'true' if args.cifar_stem else 'null'}",
           "data.synthetic=true", f"runtime.precision={args.precision}",

@@ -51,7 +51,7 @@ def _empty_nhwc(n, h, w, c, dev, dtype=torch.bfloat16):
 
 def _allreduce(t: torch.Tensor, st) -> None:
     if st.world_size > 1:
-        dist.all_reduce(t, group=st.group)
+        dist.all_reduce(t, group=st.stats_group)
 
 
 def _deliver_grad(param: torch.Tensor, compute) -> None:
@@ -195,38 +195,64 @@ class FusedStages:
                             bn.bias.detach(), ss)
         return _BNState(mi, ss.view(2, S * C), count)
 
-    def _bn_bwd(self, ops, bn, partial, nblk_seg: int, bs: _BNState, S: int, st) -> torch.Tensor:
-        """Finalize a BN backward from Σg, Σg·x̂ partials: dγ, dβ → flat grads; returns coef."""
-        C = bn.num_features
-        dev = partial.device
-        coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
-        if st.world_size == 1:
-            def run(dg, db):  # one launch: reduce + backward finalize (last-arriver)
-                ops.bn_reduce_fused(partial, nblk_seg, S, C, 2, None, bs.count, 0.0, 0.0, None,
-                                    None, bs.mi, None, bn.weight.detach(), None, None, dg, db,
-                                    coef)
-        else:
-            sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, sums)
-            _allreduce(sums, st)
-
-            def run(dg, db):
-                ops.bn_bwd_finalize(sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db,
-                                    coef)
-
+    def _deliver_bn_grads(self, bn, run) -> None:
+        """``run(dgamma_out, dbeta_out)`` writes dγ, dβ; route them into the flat store."""
         gslot = getattr(bn.weight, "_slot", None)
         bslot = getattr(bn.bias, "_slot", None)
         if gslot is not None and bslot is not None:
             run(gslot.grad, bslot.grad)
             gslot.store.mark_ready(gslot.index)
             bslot.store.mark_ready(bslot.index)
+            return
+        C = bn.num_features
+        dg = torch.empty((C,), device=bn.weight.device, dtype=torch.float32)
+        db = torch.empty((C,), device=bn.weight.device, dtype=torch.float32)
+        run(dg, db)
+        _deliver_grad(bn.weight, lambda o: o.copy_(dg))
+        _deliver_grad(bn.bias, lambda o: o.copy_(db))
+
+    def _bn_bwd_start(self, ops, bn, partial, nblk_seg: int, bs: _BNState, S: int, st):
+        """Phase 1 of a BN backward from Σg, Σg·x̂ partials.
+
+        Distributed: reduce to the LOCAL [2][S][C] sums, write dγ, dβ from them (SyncBN
+        semantics: parameter gradients are per-rank and summed by the data-parallel reducer
+        like every other gradient — using the all-reduced sums here would count them W
+        times), then start the all-reduce of the sums asynchronously; the caller schedules
+        independent work (a weight gradient) before ``_bn_bwd_finish``.  Single GPU: nothing
+        to wait for (one fused launch in the finish)."""
+        C = bn.num_features
+        if st.world_size == 1:
+            return ("local", bn, partial, nblk_seg, bs)
+        dev = partial.device
+        sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
+        ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, sums)
+        scratch = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
+        self._deliver_bn_grads(bn, lambda dg, db: ops.bn_bwd_finalize(
+            sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db, scratch))
+        work = dist.all_reduce(sums, group=st.stats_group, async_op=True)
+        return ("dist", bn, sums, work, bs)
+
+    def _bn_bwd_finish(self, ops, h, S: int) -> torch.Tensor:
+        """Phase 2: coef [3][S][C] for the input gradient (from the global sums)."""
+        bn, bs = h[1], h[4]
+        C = bn.num_features
+        dev = bs.mi.device
+        coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
+        if h[0] == "local":
+            partial, nblk_seg = h[2], h[3]
+            self._deliver_bn_grads(bn, lambda dg, db: ops.bn_reduce_fused(
+                partial, nblk_seg, S, C, 2, None, bs.count, 0.0, 0.0, None, None, bs.mi, None,
+                bn.weight.detach(), None, None, dg, db, coef))
         else:
-            dg = torch.empty((C,), device=dev, dtype=torch.float32)
-            db = torch.empty((C,), device=dev, dtype=torch.float32)
-            run(dg, db)
-            _deliver_grad(bn.weight, lambda o: o.copy_(dg))
-            _deliver_grad(bn.bias, lambda o: o.copy_(db))
+            sums, work = h[2], h[3]
+            work.wait()
+            ops.bn_bwd_finalize(sums, bs.mi, bn.weight.detach(), S, C, bs.count, None, None,
+                                coef)
         return coef
+
+    def _bn_bwd(self, ops, bn, partial, nblk_seg: int, bs: _BNState, S: int, st) -> torch.Tensor:
+        return self._bn_bwd_finish(ops, self._bn_bwd_start(ops, bn, partial, nblk_seg, bs, S, st),
+                                   S)
 
     def _wgrad(self, ops, dyn, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int):
         Nb, H, W, C = xn.shape
@@ -371,12 +397,15 @@ class FusedStages:
         return g
 
     def _block_backward(self, ops, st, S, b: _BlockSpec, tp: _BlockTape, g: torch.Tensor,
-                        pre: Optional[Tuple[torch.Tensor, int]], prev):
+                        pre, prev):
         """``g`` = dL/d(block output).  ``pre = None``: g is the raw gradient; otherwise g is
-        already ReLU-masked and ``pre`` holds the last BN's Σg, Σg·x̂ partials (computed by the
-        following block's dgrad epilogue).  Returns the same pair for the block input: masked +
-        partials when the producer is another block of this executor (``prev``), raw
-        otherwise."""
+        already ReLU-masked and ``pre`` is the started BN backward (``_bn_bwd_start``) of this
+        block's last BN, whose Σg, Σg·x̂ partials the following block's dgrad epilogue
+        produced.  Returns the same pair for the block input: masked + started when the
+        producer is another block of this executor (``prev``), raw otherwise.
+
+        Every BN all-reduce (distributed) is started before an independent weight-gradient
+        kernel and finished after it, so its latency hides behind the wgrad."""
         out = tp.out
         L = len(b.convs) - 1
         aL, bsL = tp.acts[L], tp.bns[L]
@@ -392,9 +421,8 @@ class FusedStages:
             g3 = torch.empty_like(out)
             ops.bn_bwd_apply(g, out, aL, coefL, S, True, da, g3)  # g3 = g·[out > 0]
         else:
-            partial, nblk = pre
             g3 = g
-            coefL = self._bn_bwd(ops, b.convs[L].bn, partial, nblk, bsL, S, st)
+            coefL = self._bn_bwd_finish(ops, pre, S)
             ops.bn_bwd_apply(g3, None, aL, coefL, S, False, da, None)
         dad = None
         if b.down is not None:
@@ -404,31 +432,37 @@ class FusedStages:
             coefd = self._bn_bwd(ops, b.down.bn, partial_d, nblk_d, tp.bnd, S, st)
             dad = torch.empty_like(tp.ad)
             ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
-        # conv chain, last to first
+        # conv chain, last to first: dgrad (+ BN-bwd partials) → start BN all-reduce → wgrad →
+        # finish BN → apply
         for i in range(L, 0, -1):
             cs = b.convs[i]
             xin, pro_ss = tp.ins[i]
-            self._wgrad(ops, da, xin, cs, pro_ss, S)
             a_prev, bs_prev = tp.acts[i - 1], tp.bns[i - 1]
             gm, part, nb = self._dgrad(ops, da, cs, a_prev.shape, S, bn_epi=("mask", a_prev, bs_prev))
-            coef = self._bn_bwd(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
-            da = torch.empty_like(a_prev)
-            ops.bn_bwd_apply(gm, None, a_prev, coef, S, False, da, None)
+            h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
+            self._wgrad(ops, da, xin, cs, pro_ss, S)
+            coef = self._bn_bwd_finish(ops, h, S)
+            da_next = torch.empty_like(a_prev)
+            ops.bn_bwd_apply(gm, None, a_prev, coef, S, False, da_next, None)
+            da = da_next
         cs0 = b.convs[0]
-        self._wgrad(ops, da, tp.x, cs0, None, S)
         if b.down is not None:
-            self._wgrad(ops, dad, tp.x, b.down, None, S)
             resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
         else:
             resid = g3
         if prev is None:
             dx, _, _ = self._dgrad(ops, da, cs0, tp.x.shape, S, accumulate=True, dx=resid)
-            return dx, None
-        pb, ptp = prev
-        dx = resid if b.down is not None else None
-        gx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S, dx=dx,
-                                   bn_epi=("res", resid, tp.x, ptp.acts[-1], ptp.bns[-1].mi))
-        return gx, (part, nb)
+            h = None
+        else:
+            pb, ptp = prev
+            dx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S,
+                                       dx=resid if b.down is not None else None,
+                                       bn_epi=("res", resid, tp.x, ptp.acts[-1], ptp.bns[-1].mi))
+            h = self._bn_bwd_start(ops, pb.convs[-1].bn, part, nb, ptp.bns[-1], S, st)
+        self._wgrad(ops, da, tp.x, cs0, None, S)
+        if b.down is not None:
+            self._wgrad(ops, dad, tp.x, b.down, None, S)
+        return dx, h
 
 
 class FusedStagesFn(torch.autograd.Function):

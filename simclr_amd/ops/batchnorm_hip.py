@@ -34,7 +34,7 @@ def _empty_like_cl(x: torch.Tensor) -> torch.Tensor:
 
 def _allreduce(t: torch.Tensor, st) -> None:
     if st.world_size > 1:
-        dist.all_reduce(t, group=st.group)
+        dist.all_reduce(t, group=st.stats_group)
 
 
 def _grad_out(param: torch.Tensor):
@@ -103,10 +103,13 @@ class BatchNormHipFn(torch.autograd.Function):
             ops.bn_reduce_fused(partial, nblk, S, C, 2, None, count, 0.0, 0.0, None, None, mi,
                                 None, weight.detach(), None, None, dgamma, dbeta, coef)
         else:
+            # dγ, dβ from the LOCAL sums (the data-parallel reducer sums them across ranks,
+            # as SyncBatchNorm + DDP do); the input gradient needs the global sums
             sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
             ops.bn_reduce_fused(partial, nblk, S, C, 0, sums)
-            _allreduce(sums, st)
             ops.bn_bwd_finalize(sums, mi, weight.detach(), S, C, count, dgamma, dbeta, coef)
+            _allreduce(sums, st)
+            ops.bn_bwd_finalize(sums, mi, weight.detach(), S, C, count, None, None, coef)
         if gslot is not None:
             gslot.store.mark_ready(gslot.index)
         if bslot is not None:

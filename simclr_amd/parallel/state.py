@@ -20,6 +20,13 @@ class ParallelState:
     local_rank: int = 0
     group: Optional[object] = None
     backend: str = "none"
+    # second communicator for the latency-critical BatchNorm statistics all-reduces, so they
+    # never queue behind a multi-MiB gradient-bucket all-reduce on the same RCCL stream
+    stat_group: Optional[object] = None
+
+    @property
+    def stats_group(self):
+        return self.stat_group if self.stat_group is not None else self.group
 
     @property
     def distributed(self) -> bool:
@@ -37,6 +44,12 @@ def set_state(**kw) -> ParallelState:
     for k, v in kw.items():
         setattr(_STATE, k, v)
     return _STATE
+
+
+def make_stat_group(st: "ParallelState") -> None:
+    """Create the BN-statistics communicator (collective call: every rank, same order)."""
+    if st.world_size > 1 and st.stat_group is None and dist.is_initialized():
+        st.stat_group = dist.new_group(list(range(st.world_size)))
 
 
 def reset() -> None:

@@ -63,6 +63,7 @@ def init_distributed(cfg=None, use_cuda: bool = True, backend: Optional[str] = N
                           group=dist.group.WORLD if world > 1 else None,
                           backend=(dist.get_backend() if world > 1 else "none"))
     st.device = device
+    pstate.make_stat_group(st)
     return st
 
 
