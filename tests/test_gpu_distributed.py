@@ -32,10 +32,21 @@ def _free_port():
 
 
 def _inputs():
+    # per-image contrast / brightness so the features differ across the batch (iid uniform
+    # noise images make every embedding nearly identical, which BN turns into pure rounding
+    # noise — see the docstring)
     g = torch.Generator().manual_seed(11)
     n = N_PER_RANK * WORLD
-    v0 = torch.rand(n, 8, 32, 32, generator=g)
-    v1 = torch.rand(n, 8, 32, 32, generator=g)
+
+    def imgs():
+        s = 0.2 + 0.8 * torch.rand(n, 1, 1, 1, generator=g)
+        t = 0.5 * torch.rand(n, 3, 1, 1, generator=g)
+        lo = torch.rand(n, 3, 4, 4, generator=g).repeat_interleave(8, 2).repeat_interleave(8, 3)
+        x = (s * (0.5 * lo + 0.5 * torch.rand(n, 3, 32, 32, generator=g)) + t).clamp(0, 1)
+        return torch.cat([x, torch.zeros(n, 5, 32, 32)], 1)
+
+    v0 = imgs()
+    v1 = imgs()
     w0 = torch.randn(n, D, generator=g)
     w1 = torch.randn(n, D, generator=g)
     return v0, v1, w0, w1
@@ -47,6 +58,10 @@ def _build(dev, fused=True):
     torch.manual_seed(0)
     m = ContrastiveModel(base_cnn="resnet50", d=D, cifar_stem=True).to(dev)
     m.f.use_fused_stages = fused
+    with torch.no_grad():  # damped residual branches: a better-conditioned network at init
+        for layer in (m.f.layer1, m.f.layer2, m.f.layer3, m.f.layer4):
+            for blk in layer:
+                blk.bn3.weight.mul_(0.2)
     store = FlatParamStore(m, dev, shadow_dtype=torch.bfloat16, bucket_mb=4.0,
                            first_bucket_mb=1.0)
     m.train()
@@ -143,11 +158,17 @@ def test_two_ranks_match_one_process(tmp_path, fused):
 
     noise_h, dist_h = rel(hB, hA), rel(zd, hA)
     noise_g, dist_g = rel(gB[keep], gA[keep]), rel(got["grad"][keep], gA[keep])
+    bn = torch.zeros_like(gA, dtype=torch.bool)  # BN γ/β only: catches mis-scaled SyncBN grads
+    for (o, n_), name in zip(got["segs"], got["names"]):
+        if name.startswith("f.") and ("bn" in name or "downsample.1" in name):
+            bn[o:o + n_] = True
+    noise_bn, dist_bn = rel(gB[bn], gA[bn]), rel(got["grad"][bn], gA[bn])
     noise_rs = max(rel(a, b) for a, b in zip(rsB, rsA))
     dist_rs = max(rel(a, b) for a, b in zip(got["rs"], rsA))
     msg = dict(noise_h=noise_h, dist_h=dist_h, noise_g=noise_g, dist_g=dist_g,
-               noise_rs=noise_rs, dist_rs=dist_rs)
+               noise_bn=noise_bn, dist_bn=dist_bn, noise_rs=noise_rs, dist_rs=dist_rs)
     print("DIST-CHECK", msg)
     assert dist_h <= 3 * noise_h + 2e-3, msg
     assert dist_g <= 3 * noise_g + 2e-3, msg
+    assert dist_bn <= 3 * noise_bn + 2e-3, msg
     assert dist_rs <= 3 * noise_rs + 2e-3, msg

@@ -18,6 +18,13 @@ def run(mode, x, w, base="resnet50", stem=True, perm=None):
     torch.manual_seed(0)
     m = ContrastiveModel(base_cnn=base, d=128, cifar_stem=stem).to(dev)
     m.f.use_fused_stages = mode == "fused"
+    damp = float(os.environ.get("DAMP", "1.0"))
+    if damp != 1.0:  # damped residual branches: a well-conditioned (near-identity) network
+        with torch.no_grad():
+            for layer in (m.f.layer1, m.f.layer2, m.f.layer3, m.f.layer4):
+                for blk in layer:
+                    last = blk.bn3 if hasattr(blk, "bn3") else blk.bn2
+                    last.weight.mul_(damp)
     store = FlatParamStore(m, dev, shadow_dtype=torch.bfloat16)
     m.train()
     if mode == "fp32":

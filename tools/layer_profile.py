@@ -1,0 +1,103 @@
+"""Per-op timing of one SimCLR training step with semantic labels (conv shape / pass / fusion
+mode), using HIP events around every ``torch.ops.simclr_amd`` call.
+
+Usage (GPU box): python tools/layer_profile.py [--batch 512] [--steps 3] > out.md
+Every op is bracketed by events on the current stream (no extra synchronisation inside the
+step), so the numbers are the kernels' own durations in their real order."""
+import argparse
+import os
+import sys
+from collections import defaultdict
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class _Timed:
+    def __init__(self, real, log):
+        self._real = real
+        self._log = log
+
+    def __getattr__(self, name):
+        f = getattr(self._real, name)
+        if not callable(f) or name.endswith(("variants", "_bm", "_bn", "splits", "blocks")):
+            return f
+
+        def wrap(*args, **kw):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = f(*args, **kw)
+            e.record()
+            self._log.append((_label(name, args), s, e))
+            return r
+        return wrap
+
+
+def _label(name, args):
+    if name == "igemm":
+        g = args[5]
+        M = g[0] * g[4] * g[5]
+        K = g[6] * g[7] * g[3]
+        mode = args[10] if len(args) > 10 else 0
+        pro = args[6] is not None
+        kind = "fwd" if g[10] == 1 and g[12] <= 0 and g[17] == 1 else "dgrad"
+        return f"igemm {kind} M={M} N={g[14]} K={K} k={g[6]} s={g[8]}{' pro' if pro else ''} epi{mode}", 2.0 * M * g[14] * K
+    if name == "wgrad":
+        g = args[4]
+        M = g[0] * g[4] * g[5]
+        K = g[6] * g[7] * g[3]
+        return f"wgrad M={M} N={g[14]} K={K} k={g[6]}{' pro' if args[8] is not None else ''}", 2.0 * M * g[14] * K
+    shape = tuple(args[0].shape) if hasattr(args[0], "shape") else ""
+    return f"{name} {shape}", 0.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    from simclr_amd.ops import _ext
+    from simclr_amd.config import compose, task_config, CONF_DIR
+    from simclr_amd.data.datasets import synthetic_dataset
+    from simclr_amd.data.loader import ContrastiveLoader
+    from simclr_amd.parallel import state as pstate
+    from simclr_amd.train.pretrain import Trainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    st = pstate.get()
+    st.device = dev
+    cfg = task_config(compose(str(CONF_DIR), "config", [
+        "experiment.base_cnn=resnet50", "model.cifar_stem=true", f"experiment.batches={a.batch}",
+        "data.synthetic=true", "parameter.epochs=10"]))
+    tr = Trainer(cfg, st, 50000)
+    loader = ContrastiveLoader(synthetic_dataset(4096, 10), a.batch, dev, seed=7)
+    it = iter(loader)
+    for _ in range(2):  # warm-up + autotune
+        tr.step(next(it)[0])
+    torch.cuda.synchronize()
+    log = []
+    real = _ext.ops()
+    timed = _Timed(real, log)
+    _ext.ops = lambda: timed
+    for _ in range(a.steps):
+        tr.step(next(it)[0])
+    torch.cuda.synchronize()
+    agg = defaultdict(lambda: [0, 0.0, 0.0])
+    for (lab, flops), s, e in log:
+        v = agg[lab]
+        v[0] += 1
+        v[1] += s.elapsed_time(e) * 1e3
+        v[2] += flops
+    tot = sum(v[1] for v in agg.values()) / a.steps
+    print(f"# per-op time, ResNet-50 CIFAR, batch {a.batch}x2 views, avg of {a.steps} steps\n")
+    print(f"total timed op time/step: {tot / 1e3:.2f} ms\n")
+    print("| op | calls/step | us/step | % | TF/s |\n|---|---:|---:|---:|---:|")
+    for lab, (n, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        tf = f"{fl / (t * 1e-6) / 1e12:.0f}" if fl else ""
+        print(f"| {lab} | {n / a.steps:.1f} | {t / a.steps:.1f} | {100 * t / a.steps / tot:.1f} | {tf} |")
+
+
+if __name__ == "__main__":
+    main()
