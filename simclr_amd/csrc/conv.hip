@@ -83,7 +83,7 @@ __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const fl
 }
 
 template <int BM, int BN, int WM, int WN, bool PRO, int EPI>
-__global__ __launch_bounds__(256, 2) void igemm_nt(IgemmArgs p) {
+__global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(IgemmArgs p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / 256;
@@ -374,7 +374,7 @@ struct WgradArgs {
 };
 
 template <int BCO, int BKK, int WM, int WN, bool PRO>
-__global__ __launch_bounds__(256, 2) void wgrad_tn(WgradArgs p) {
+__global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn(WgradArgs p) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
   constexpr int FM = TCO / 16, FN = TKK / 16;
   constexpr int SD = BCO + 8;   // LDS row stride (elements) of the dY tile
@@ -688,8 +688,11 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
 }
 
 // tile variants: {BM, BN}
-constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {64, 64}};
-constexpr int WG_VARIANTS[][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+// wide-N / wide-K tiles (5, 6 and wgrad 4, 5) cover a whole small output dimension in one tile,
+// so the other operand is streamed from HBM once instead of N/BN (K/BKK) times
+constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {64, 64},
+                                  {128, 256}, {64, 256}};
+constexpr int WG_VARIANTS[][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {64, 256}, {256, 64}};
 
 }  // namespace
 
@@ -725,6 +728,8 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
     case 3: launch_igemm<64, 128, 2, 2>(a, s); break;
+    case 5: launch_igemm<128, 256, 2, 2>(a, s); break;
+    case 6: launch_igemm<64, 256, 1, 4>(a, s); break;
     default: launch_igemm<64, 64, 2, 2>(a, s); break;
   }
 }
@@ -769,6 +774,8 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;
+    case 4: launch_wgrad<64, 256, 2, 2>(a, s); break;
+    case 5: launch_wgrad<256, 64, 2, 2>(a, s); break;
     default: launch_wgrad<64, 64, 2, 2>(a, s); break;
   }
   const int K = a.K;
