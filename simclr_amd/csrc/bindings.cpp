@@ -90,7 +90,8 @@ ConvFusion fusion_from(const c10::optional<Tensor>& pro_sc, const c10::optional<
   TORCH_CHECK(epi_mode >= 0 && epi_mode <= 4, "epi_mode");
   if (epi_mode == 1 || epi_mode == 2 || epi_mode == 4)
     TORCH_CHECK(f.epi_a && epi_a->numel() >= out_numel, "epilogue operand a");
-  if (epi_mode >= 2) TORCH_CHECK(f.epi_b && epi_b->numel() >= out_numel, "epilogue operand b");
+  if (epi_mode == 2 || epi_mode == 3)
+    TORCH_CHECK(f.epi_b && epi_b->numel() >= out_numel, "epilogue operand b");
   return f;
 }
 
@@ -101,7 +102,8 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const c10::optional<Tensor>& epi_a, const c10::optional<Tensor>& epi_b,
            int64_t variant, const c10::optional<Tensor>& epi_ss,
            const c10::optional<Tensor>& epi_mi, int64_t seg_rows, int64_t stats_seg_blocks,
-           int64_t stats_base, const c10::optional<Tensor>& epi_c) {
+           int64_t stats_base, const c10::optional<Tensor>& epi_c,
+           const c10::optional<Tensor>& epi_mask) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -148,6 +150,11 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
     } else {
       f.epi_c = optbf(epi_c, "epi_c");
       TORCH_CHECK(f.epi_c && epi_c->numel() >= out.numel(), "igemm mode 4: epilogue operand c");
+      if (epi_mask.has_value() && epi_mask->defined()) {
+        check_dev(*epi_mask, at::kByte, "epi_mask");
+        TORCH_CHECK(epi_mask->numel() * 8 >= out.numel(), "igemm mode 4: mask size");
+        f.epi_mask = epi_mask->data_ptr<uint8_t>();
+      }
     }
   }
   if (f.pro_sc) {
@@ -327,7 +334,8 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
 }
 
 void bn_apply_ss_op(const Tensor& x, const Tensor& ss, const c10::optional<Tensor>& res,
-                    const c10::optional<Tensor>& rss, const Tensor& y, int64_t S, bool relu) {
+                    const c10::optional<Tensor>& rss, const Tensor& y, int64_t S, bool relu,
+                    const c10::optional<Tensor>& mask) {
   check_rc(x, S, "bn_apply_ss");
   const int C = x.size(-1), R = x.numel() / C;
   TORCH_CHECK(y.numel() == x.numel(), "bn_apply_ss: y size");
@@ -336,8 +344,14 @@ void bn_apply_ss_op(const Tensor& x, const Tensor& ss, const c10::optional<Tenso
   if (has_res) TORCH_CHECK(res->numel() == x.numel(), "bn_apply_ss: res size");
   if (rss.has_value() && rss->defined())
     TORCH_CHECK(has_res && rss->numel() >= 2 * S * C, "bn_apply_ss: rss needs res, [2][S][C]");
-  bn_apply_ss(bf(x, "x"), f32(ss, "ss"), optbf(res, "res"), optf32(rss, "rss"), bfw(y, "y"), R, C,
-              S, relu ? 1 : 0, cur_stream());
+  uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    check_dev(*mask, at::kByte, "mask");
+    TORCH_CHECK(mask->numel() * 8 == x.numel(), "bn_apply_ss: mask must be [R][C/8] uint8");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  bn_apply_ss(bf(x, "x"), f32(ss, "ss"), optbf(res, "res"), optf32(rss, "rss"), bfw(y, "y"), mk, R,
+              C, S, relu ? 1 : 0, cur_stream());
 }
 
 void bn_apply_op(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& y,
@@ -536,7 +550,7 @@ void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int6
 }  // namespace
 
 TORCH_LIBRARY(simclr_amd, m) {
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None) -> ()", &igemm);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
   m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);
@@ -550,7 +564,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
   m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
   m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None) -> ()", &bn_reduce_fused_op);
-  m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu) -> ()", &bn_apply_ss_op);
+  m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);
   m.def("bn_bwd_reduce(Tensor dy, Tensor? y, Tensor x, Tensor mi, int S, bool relu, Tensor(a!) partial) -> ()", &bn_bwd_reduce_op);

@@ -388,8 +388,9 @@ __global__ __launch_bounds__(256) void k_bn_apply_ss(const uint16_t* __restrict_
                                                      const float* __restrict__ ss,
                                                      const uint16_t* __restrict__ res,
                                                      const float* __restrict__ rss,
-                                                     uint16_t* __restrict__ y, int R, int C, int S,
-                                                     int relu) {
+                                                     uint16_t* __restrict__ y,
+                                                     uint8_t* __restrict__ mask, int R, int C,
+                                                     int S, int relu) {
   const int CH = C / 8;
   const int TPR = CH < 256 ? CH : 256;
   const int RPB = 256 / TPR;
@@ -447,6 +448,12 @@ __global__ __launch_bounds__(256) void k_bn_apply_ss(const uint16_t* __restrict_
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = pack2bf(o[2 * e], o[2 * e + 1]);
         *(u32x4*)(y + sbase + (size_t)r * C + cc * 8) = w;
+        if (mask != nullptr) {  // bit e = (y[c0 + e] > 0): the ReLU mask at 1/16 of y's bytes
+          unsigned bits = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bits |= (o[e] > 0.f ? 1u : 0u) << e;
+          mask[(sbase + (size_t)r * C) / 8 + cc] = (uint8_t)bits;
+        }
       }
     }
   }
@@ -746,14 +753,17 @@ void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s) {
 }
 
 void bn_apply_ss(const uint16_t* x, const float* ss, const uint16_t* res, const float* rss,
-                 uint16_t* y, int R, int C, int S, int relu, hipStream_t s) {
+                 uint16_t* y, uint8_t* mask, int R, int C, int S, int relu, hipStream_t s) {
   const dim3 grid(apply_grid(R, C, S), S);
   if (res == nullptr)
-    hipLaunchKernelGGL(k_bn_apply_ss<0>, grid, dim3(256), 0, s, x, ss, res, rss, y, R, C, S, relu);
+    hipLaunchKernelGGL(k_bn_apply_ss<0>, grid, dim3(256), 0, s, x, ss, res, rss, y, mask, R, C, S,
+                       relu);
   else if (rss == nullptr)
-    hipLaunchKernelGGL(k_bn_apply_ss<1>, grid, dim3(256), 0, s, x, ss, res, rss, y, R, C, S, relu);
+    hipLaunchKernelGGL(k_bn_apply_ss<1>, grid, dim3(256), 0, s, x, ss, res, rss, y, mask, R, C, S,
+                       relu);
   else
-    hipLaunchKernelGGL(k_bn_apply_ss<2>, grid, dim3(256), 0, s, x, ss, res, rss, y, R, C, S, relu);
+    hipLaunchKernelGGL(k_bn_apply_ss<2>, grid, dim3(256), 0, s, x, ss, res, rss, y, mask, R, C, S,
+                       relu);
   HIP_CHECK_LAUNCH();
 }
 

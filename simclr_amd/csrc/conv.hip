@@ -58,6 +58,7 @@ struct IgemmArgs {
   const uint16_t* epi_a;
   const uint16_t* epi_b;
   const uint16_t* epi_c;
+  const uint8_t* epi_mask;  // mode 4: ReLU bitmask (bit e of byte o/8) instead of epi_b
   const float* epi_ss;  // mode 3: [2][S][N] BN scale / shift
   const float* epi_mi;  // mode 3/4: [2][S][N] BN mean / invstd
   int epi_S;
@@ -308,13 +309,21 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
       }
     } else if (EPI == 4) {
       const u32x4 r = *(const u32x4*)(p.epi_a + o);
-      const u32x4 y = *(const u32x4*)(p.epi_b + o);
       const u32x4 xa = *(const u32x4*)(p.epi_c + o);
+      unsigned bits = 0;
+      if (p.epi_mask != nullptr) {
+        bits = p.epi_mask[o >> 3];
+      } else {
+        const u32x4 y = *(const u32x4*)(p.epi_b + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bits |= (lo_bf(y[e]) > 0.f ? 1u : 0u) << (2 * e) | (hi_bf(y[e]) > 0.f ? 2u : 0u) << (2 * e);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const uint32_t sum = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
-        const float g0 = lo_bf(y[e]) > 0.f ? lo_bf(sum) : 0.f;
-        const float g1 = hi_bf(y[e]) > 0.f ? hi_bf(sum) : 0.f;
+        const float g0 = (bits >> (2 * e)) & 1u ? lo_bf(sum) : 0.f;
+        const float g1 = (bits >> (2 * e + 1)) & 1u ? hi_bf(sum) : 0.f;
         v[e] = pack2bf(g0, g1);
         if (p.stats != nullptr) {
           s1[2 * e] += g0; s2[2 * e] += g0 * ((lo_bf(xa[e]) - emu[2 * e]) * einv[2 * e]);
@@ -720,6 +729,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh; a.pro_seg_rows = f.pro_seg_rows > 0 ? f.pro_seg_rows : a.M;
   a.pro_relu = f.pro_relu;
   a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b; a.epi_c = f.epi_c;
+  a.epi_mask = f.epi_mask;
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);

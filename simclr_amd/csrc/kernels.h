@@ -30,6 +30,7 @@ struct ConvFusion {
   const uint16_t* epi_a = nullptr;
   const uint16_t* epi_b = nullptr;
   const uint16_t* epi_c = nullptr;  // mode 4: pre-BN activation for x̂
+  const uint8_t* epi_mask = nullptr;  // mode 4: ReLU bitmask of the block input (see bn_apply_ss)
   const float* epi_ss = nullptr;  // mode 3: [2][S][N] scale/shift
   const float* epi_mi = nullptr;  // mode 3/4: [2][S][N] mean/invstd
   int epi_S = 1;
@@ -86,8 +87,9 @@ struct BnReduceFusedParams {
 };
 void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s);
 // y = relu?(x*sc + sh + [res | res*rsc + rsh]); ss / rss are [2][S][C] scale/shift tables
+// optional mask: uint8 [R][C/8], bit e of byte (r, c/8) = (y[r][c] > 0)
 void bn_apply_ss(const uint16_t* x, const float* ss, const uint16_t* res, const float* rss,
-                 uint16_t* y, int R, int C, int S, int relu, hipStream_t s);
+                 uint16_t* y, uint8_t* mask, int R, int C, int S, int relu, hipStream_t s);
 void bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* mean_invstd,
               const float* gamma, const float* beta, int R, int C, int S, int relu,
               hipStream_t s);

@@ -106,6 +106,7 @@ class _BlockTape:
     ad: Optional[torch.Tensor] = None
     bnd: Optional[_BNState] = None
     out: Optional[torch.Tensor] = None
+    mask: Optional[torch.Tensor] = None  # uint8 ReLU bitmask of ``out`` (bit per channel)
 
 
 class FusedStages:
@@ -272,9 +273,9 @@ class FusedStages:
         ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
         (segment-major across stride-2 parity classes) → (dx, partial, blocks_per_segment):
           ("mask", a_prev, bn_state)      mode 3: g = dx·[bn(a_prev) > 0] (BN+ReLU producer)
-          ("res", resid, y, a_prev, mi)   mode 4: g = (dx + resid)·[y > 0] (residual-block
-                                          producer: y = its output, a_prev = its last pre-BN
-                                          activation); resid may alias dx (in-place add)
+          ("res", resid, mask, a_prev, mi) mode 4: g = (dx + resid)·[y > 0] (residual-block
+                                          producer: mask = its output's ReLU bitmask, a_prev =
+                                          its last pre-BN activation); resid may alias dx
         """
         Nb, H, W, Ci = in_shape
         _, OH, OW, Co = dyn.shape
@@ -327,8 +328,8 @@ class FusedStages:
             epi = (3, None, a_prev)
             tables = (bs.ss.view(-1), bs.mi)
         else:
-            _, resid, y, a_prev, mi = bn_epi
-            epi = (4, resid, y, a_prev)
+            _, resid, mask, a_prev, mi = bn_epi
+            epi = (4, resid, None, a_prev, mask)
             tables = (None, mi)
         chosen = []
         for wt, g, M in launches:
@@ -373,15 +374,18 @@ class FusedStages:
                 cur, pro_ss = a, bs.ss
             aL, bsL = tp.acts[-1], tp.bns[-1]
             out = torch.empty_like(aL)
+            # the next block's input-gradient epilogue only needs [out > 0]: 1 bit per element
+            mask = torch.empty((aL.numel() // 8,), device=aL.device, dtype=torch.uint8)
             if b.down is not None:
                 ad, partial, nblk = self._conv_fwd(ops, x, b.down, None, S)
                 rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
                 tp.ad = ad
                 tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st)
-                ops.bn_apply_ss(aL, bsL.ss, ad, tp.bnd.ss, out, S, True)
+                ops.bn_apply_ss(aL, bsL.ss, ad, tp.bnd.ss, out, S, True, mask)
             else:
-                ops.bn_apply_ss(aL, bsL.ss, x, None, out, S, True)
+                ops.bn_apply_ss(aL, bsL.ss, x, None, out, S, True, mask)
             tp.out = out
+            tp.mask = mask
             tapes.append(tp)
             x = out
         return x, tapes
@@ -457,7 +461,7 @@ class FusedStages:
             pb, ptp = prev
             dx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S,
                                        dx=resid if b.down is not None else None,
-                                       bn_epi=("res", resid, tp.x, ptp.acts[-1], ptp.bns[-1].mi))
+                                       bn_epi=("res", resid, ptp.mask, ptp.acts[-1], ptp.bns[-1].mi))
             h = self._bn_bwd_start(ops, pb.convs[-1].bn, part, nb, ptp.bns[-1], S, st)
         self._wgrad(ops, da, tp.x, cs0, None, S)
         if b.down is not None:

@@ -52,13 +52,14 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
         default = cands[0]
     key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
+    em = epi[4] if epi is not None and len(epi) > 4 else None
 
     def trial(v):
         bm = ops.igemm_variant_bm(v)
         st = (torch.empty(((M + bm - 1) // bm) * 2 * N, device=out.device, dtype=torch.float32)
               if want_stats else None)
         ops.igemm(A, B, torch.empty_like(out), bias, st, geom, psc, psh, pseg, prelu, emode, ea,
-                  eb, v, ess, emi, seg_rows, 0, 0, ec)
+                  eb, v, ess, emi, seg_rows, 0, 0, ec, em)
 
     return tuning.pick(key, cands, default, trial)
 
@@ -68,9 +69,10 @@ def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=N
     psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
+    em = epi[4] if epi is not None and len(epi) > 4 else None
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-              seg_rows, remap[0], remap[1], ec)
+              seg_rows, remap[0], remap[1], ec, em)
 
 
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):

@@ -100,6 +100,19 @@ def test_bn_apply_ss_and_finalize_table(ops, mode):
         ref = ref + res.float().view(S, R, C) * rss[0][:, None] + rss[1][:, None]
     ref = torch.relu(ref).reshape(S * R, C)
     assert _rel(y, ref) < 1e-2
+    # optional ReLU bitmask: bit e of byte (r, c // 8) == (y[r, c] > 0)
+    mask = torch.empty(S * R * C // 8, device=DEV, dtype=torch.uint8)
+    y2 = torch.empty_like(x)
+    if mode == 0:
+        ops.bn_apply_ss(x, ss, None, None, y2, S, True, mask)
+    elif mode == 1:
+        ops.bn_apply_ss(x, ss, res, None, y2, S, True, mask)
+    else:
+        ops.bn_apply_ss(x, ss, res, rss.view(-1), y2, S, True, mask)
+    assert torch.equal(y2, y)
+    bits = (y.float() > 0).view(-1, 8).to(torch.int32)
+    packed = (bits << torch.arange(8, device=DEV, dtype=torch.int32)).sum(1)
+    assert torch.equal(mask.to(torch.int32), packed)
 
 
 def _model(base, stem, device, shadow=torch.bfloat16):
