@@ -104,10 +104,15 @@ def run_ours(args, rank, world, dev):
         loss = tr.step(next_batch())
     _sync(dev, world)
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         loss = tr.step(next_batch())
+        host += time.perf_counter() - h0
     _sync(dev, world)
     t1 = time.perf_counter()
+    # host time spent issuing the steps (≈ wall time means the run is launch/CPU bound)
+    args.host_issue_ms = host / args.steps * 1000.0
     return t1 - t0, float(loss.item()) if loss is not None else float("nan")
 
 
@@ -213,6 +218,8 @@ def main(argv=None):
             "optimizer": "LARS(trust=1e-3)+SGD(m=0.9), warmup+cosine",
             "impl": args.impl,
             "hip_graph": bool(args.graph and args.impl == "ours"),
+            "host_issue_ms_per_step": (round(args.host_issue_ms, 3)
+                                       if hasattr(args, "host_issue_ms") else None),
             "final_loss": loss,
         },
     }
