@@ -103,7 +103,8 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            int64_t variant, const c10::optional<Tensor>& epi_ss,
            const c10::optional<Tensor>& epi_mi, int64_t seg_rows, int64_t stats_seg_blocks,
            int64_t stats_base, const c10::optional<Tensor>& epi_c,
-           const c10::optional<Tensor>& epi_mask) {
+           const c10::optional<Tensor>& epi_mask, const c10::optional<Tensor>& epi_c2,
+           const c10::optional<Tensor>& epi_mi2, const c10::optional<Tensor>& stats2) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -154,6 +155,14 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
         check_dev(*epi_mask, at::kByte, "epi_mask");
         TORCH_CHECK(epi_mask->numel() * 8 >= out.numel(), "igemm mode 4: mask size");
         f.epi_mask = epi_mask->data_ptr<uint8_t>();
+      }
+      if (stats2.has_value() && stats2->defined()) {
+        f.stats2 = f32w(*stats2, "stats2");
+        f.epi_c2 = optbf(epi_c2, "epi_c2");
+        f.epi_mi2 = optf32(epi_mi2, "epi_mi2");
+        TORCH_CHECK(has_stats && f.epi_c2 && f.epi_mi2 && epi_c2->numel() >= out.numel() &&
+                        epi_mi2->numel() >= 2 * nseg * g.N && stats2->numel() >= stats->numel(),
+                    "igemm mode 4: second BN stream needs c2, mi2 [2][S][N] and stats2");
       }
     }
   }
@@ -409,6 +418,17 @@ void bn_bwd_apply_op(const Tensor& dy, const c10::optional<Tensor>& y, const Ten
                bfw(dx, "dx"), optbfw(dres, "dres"), cur_stream());
 }
 
+void bn_bwd_apply2_op(const Tensor& g, const Tensor& x1, const Tensor& coef1, const Tensor& dx1,
+                      const Tensor& x2, const Tensor& coef2, const Tensor& dx2, int64_t S) {
+  check_rc(x1, S, "bn_bwd_apply2");
+  const int C = x1.size(-1), R = x1.numel() / C;
+  TORCH_CHECK(g.numel() == x1.numel() && x2.numel() == x1.numel() && dx1.numel() == x1.numel() &&
+                  dx2.numel() == x1.numel(), "bn_bwd_apply2 sizes");
+  TORCH_CHECK(coef1.numel() >= 3 * S * C && coef2.numel() >= 3 * S * C, "bn_bwd_apply2 coef");
+  bn_bwd_apply2(bf(g, "g"), bf(x1, "x1"), f32(coef1, "coef1"), bfw(dx1, "dx1"), bf(x2, "x2"),
+                f32(coef2, "coef2"), bfw(dx2, "dx2"), R, C, S, cur_stream());
+}
+
 // ------------------------------------------------------------------------------- misc
 void avgpool_fwd_op(const Tensor& x, const Tensor& y, int64_t Nb, int64_t HW, int64_t C) {
   TORCH_CHECK(C % 8 == 0 && x.numel() == Nb * HW * C && y.numel() == Nb * C, "avgpool_fwd sizes");
@@ -421,7 +441,8 @@ void avgpool_bwd_op(const Tensor& dy, const Tensor& dx, int64_t Nb, int64_t HW, 
 void colsum_op(const Tensor& x, const Tensor& out, double beta) {
   const int C = x.size(-1), R = x.numel() / C;
   TORCH_CHECK(out.numel() == C, "colsum sizes");
-  colsum_bf16(bf(x, "x"), R, C, f32w(out, "out"), (float)beta, cur_stream());
+  at::Tensor ws = at::empty({(int64_t)colsum_groups(R) * C}, out.options());
+  colsum_bf16(bf(x, "x"), R, C, f32w(out, "out"), (float)beta, ws.data_ptr<float>(), cur_stream());
 }
 void cast_to_bf16(const Tensor& x, const Tensor& y) {
   TORCH_CHECK(x.numel() == y.numel(), "cast sizes");
@@ -550,7 +571,7 @@ void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int6
 }  // namespace
 
 TORCH_LIBRARY(simclr_amd, m) {
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None) -> ()", &igemm);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
   m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);
@@ -570,6 +591,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_bwd_reduce(Tensor dy, Tensor? y, Tensor x, Tensor mi, int S, bool relu, Tensor(a!) partial) -> ()", &bn_bwd_reduce_op);
   m.def("bn_bwd_finalize(Tensor sums, Tensor mi, Tensor? gamma, int S, int C, float count, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!) coef) -> ()", &bn_bwd_final);
   m.def("bn_bwd_apply(Tensor dy, Tensor? y, Tensor x, Tensor coef, int S, bool relu, Tensor(a!) dx, Tensor(b!)? dres) -> ()", &bn_bwd_apply_op);
+  m.def("bn_bwd_apply2(Tensor g, Tensor x1, Tensor coef1, Tensor(a!) dx1, Tensor x2, Tensor coef2, Tensor(b!) dx2, int S) -> ()", &bn_bwd_apply2_op);
   m.def("avgpool_fwd(Tensor x, Tensor(a!) y, int Nb, int HW, int C) -> ()", &avgpool_fwd_op);
   m.def("avgpool_bwd(Tensor dy, Tensor(a!) dx, int Nb, int HW, int C) -> ()", &avgpool_bwd_op);
   m.def("colsum(Tensor x, Tensor(a!) out, float beta) -> ()", &colsum_op);

@@ -671,6 +671,65 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const uint16_t* __restrict
   }
 }
 
+__global__ __launch_bounds__(256) void k_bn_bwd_apply2(const uint16_t* __restrict__ g,
+                                                       const uint16_t* __restrict__ x1,
+                                                       const float* __restrict__ coef1,
+                                                       uint16_t* __restrict__ dx1,
+                                                       const uint16_t* __restrict__ x2,
+                                                       const float* __restrict__ coef2,
+                                                       uint16_t* __restrict__ dx2, int R, int C,
+                                                       int S) {
+  const int CH = C / 8;
+  const int TPR = CH < 256 ? CH : 256;
+  const int RPB = 256 / TPR;
+  const int Rs = R / S;
+  const int seg = blockIdx.y;
+  const int cc0 = threadIdx.x % TPR;
+  const int rl = threadIdx.x / TPR;
+  if (rl >= RPB) return;
+  const size_t sbase = (size_t)seg * Rs * C;
+  const size_t sbytes = (size_t)Rs * C * 2;
+  const __amdgpu_buffer_rsrc_t rg = rsrc(g + sbase, sbytes);
+  const __amdgpu_buffer_rsrc_t r1 = rsrc(x1 + sbase, sbytes);
+  const __amdgpu_buffer_rsrc_t r2 = rsrc(x2 + sbase, sbytes);
+  for (int cc = cc0; cc < CH; cc += TPR) {
+    float A1[8], B1[8], D1[8], A2[8], B2[8], D2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = cc * 8 + e;
+      A1[e] = coef1[seg * C + c]; B1[e] = coef1[(S + seg) * C + c]; D1[e] = coef1[(2 * S + seg) * C + c];
+      A2[e] = coef2[seg * C + c]; B2[e] = coef2[(S + seg) * C + c]; D2[e] = coef2[(2 * S + seg) * C + c];
+    }
+    for (int r0 = blockIdx.x * RPB * UNR + rl; r0 < Rs; r0 += gridDim.x * RPB * UNR) {
+      u32x4 vg[UNR], v1[UNR], v2[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const uint32_t off = (uint32_t)(((size_t)(r0 + u * RPB) * C + cc * 8) * 2);
+        vg[u] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
+        v1[u] = __builtin_amdgcn_raw_buffer_load_b128(r1, off, 0, 0);
+        v2[u] = __builtin_amdgcn_raw_buffer_load_b128(r2, off, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * RPB;
+        if (r >= Rs) break;
+        u32x4 w1, w2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g0 = lo_bf(vg[u][e]), g1 = hi_bf(vg[u][e]);
+          w1[e] = pack2bf(A1[2 * e] * g0 + B1[2 * e] * lo_bf(v1[u][e]) + D1[2 * e],
+                          A1[2 * e + 1] * g1 + B1[2 * e + 1] * hi_bf(v1[u][e]) + D1[2 * e + 1]);
+          w2[e] = pack2bf(A2[2 * e] * g0 + B2[2 * e] * lo_bf(v2[u][e]) + D2[2 * e],
+                          A2[2 * e + 1] * g1 + B2[2 * e + 1] * hi_bf(v2[u][e]) + D2[2 * e + 1]);
+        }
+        const size_t off = sbase + (size_t)r * C + cc * 8;
+        *(u32x4*)(dx1 + off) = w1;
+        *(u32x4*)(dx2 + off) = w2;
+      }
+    }
+  }
+}
+
 int apply_grid(int R, int C, int S) {
   const int CH = C / 8;
   const int TPR = CH < 256 ? CH : 256;
@@ -805,5 +864,13 @@ void bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, cons
                   int R, int C, int S, int relu, uint16_t* dx, uint16_t* dres, hipStream_t s) {
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(apply_grid(R, C, S), S), dim3(256), 0, s, dy, y, x, coef, R, C,
                      S, relu, dx, dres);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_bwd_apply2(const uint16_t* g, const uint16_t* x1, const float* coef1, uint16_t* dx1,
+                   const uint16_t* x2, const float* coef2, uint16_t* dx2, int R, int C, int S,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_bwd_apply2, dim3(apply_grid(R, C, S), S), dim3(256), 0, s, g, x1, coef1,
+                     dx1, x2, coef2, dx2, R, C, S);
   HIP_CHECK_LAUNCH();
 }

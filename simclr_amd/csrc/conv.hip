@@ -59,6 +59,9 @@ struct IgemmArgs {
   const uint16_t* epi_b;
   const uint16_t* epi_c;
   const uint8_t* epi_mask;  // mode 4: ReLU bitmask (bit e of byte o/8) instead of epi_b
+  const uint16_t* epi_c2;   // mode 4: second pre-BN activation (the producer's downsample BN)
+  const float* epi_mi2;     //   its mean / invstd [2][S][N]
+  float* stats2;            //   its partials Σg, Σg·x̂2 (same row layout as stats)
   const float* epi_ss;  // mode 3: [2][S][N] BN scale / shift
   const float* epi_mi;  // mode 3/4: [2][S][N] BN mean / invstd
   int epi_S;
@@ -247,13 +250,14 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
   constexpr int RSTEP = 256 / CPR;       // rows per pass
   const int ch = tid % CPR;
   const int r0 = tid / CPR;
-  float s1[8], s2[8];
+  float s1[8], s2[8], s3[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+  constexpr bool two = EPI == 5;  // mode 4 + the producer's downsample-BN stream
   const int n = n0 + ch * 8;
   const int seg = p.seg_rows > 0 ? m0 / p.seg_rows : 0;  // block-uniform (host guarantees)
-  float esc[8], esh[8], emu[8], einv[8];
-  if (EPI == 3 || EPI == 4) {
+  float esc[8], esh[8], emu[8], einv[8], emu2[8], einv2[8];
+  if (EPI == 3 || EPI == 4 || EPI == 5) {
     const int S = p.epi_S;
     const int cb = n < p.N ? n : 0;
 #pragma unroll
@@ -264,6 +268,10 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
       }
       emu[e] = p.epi_mi[seg * p.N + cb + e];
       einv[e] = p.epi_mi[(S + seg) * p.N + cb + e];
+      if (two) {
+        emu2[e] = p.epi_mi2[seg * p.N + cb + e];
+        einv2[e] = p.epi_mi2[(S + seg) * p.N + cb + e];
+      }
     }
   }
   for (int row = r0; row < BM; row += RSTEP) {
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
           s1[2 * e + 1] += g1; s2[2 * e + 1] += g1 * ((y1 - emu[2 * e + 1]) * einv[2 * e + 1]);
         }
       }
-    } else if (EPI == 4) {
+    } else if (EPI == 4 || EPI == 5) {
       const u32x4 r = *(const u32x4*)(p.epi_a + o);
       const u32x4 xa = *(const u32x4*)(p.epi_c + o);
       unsigned bits = 0;
@@ -331,9 +339,18 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
           s2[2 * e + 1] += g1 * ((hi_bf(xa[e]) - emu[2 * e + 1]) * einv[2 * e + 1]);
         }
       }
+      if (two) {
+        const u32x4 xd = *(const u32x4*)(p.epi_c2 + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g0 = lo_bf(v[e]), g1 = hi_bf(v[e]);
+          s3[2 * e] += g0 * ((lo_bf(xd[e]) - emu2[2 * e]) * einv2[2 * e]);
+          s3[2 * e + 1] += g1 * ((hi_bf(xd[e]) - emu2[2 * e + 1]) * einv2[2 * e + 1]);
+        }
+      }
     }
     *(u32x4*)(p.out + o) = v;
-    if (EPI != 3 && EPI != 4 && p.stats != nullptr) {
+    if (EPI < 3 && p.stats != nullptr) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float a = lo_bf(v[e]), b = hi_bf(v[e]);
@@ -344,24 +361,31 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
   }
   if (p.stats != nullptr) {
     __syncthreads();
-    float* red = (float*)smem;  // [RSTEP][BN][2]
+    constexpr int NS = two ? 3 : 2;
+    float* red = (float*)smem;  // [RSTEP][BN][NS]
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[(r0 * BN + ch * 8 + e) * 2 + 0] = s1[e];
-      red[(r0 * BN + ch * 8 + e) * 2 + 1] = s2[e];
+      red[(r0 * BN + ch * 8 + e) * NS + 0] = s1[e];
+      red[(r0 * BN + ch * 8 + e) * NS + 1] = s2[e];
+      if (two) red[(r0 * BN + ch * 8 + e) * NS + 2] = s3[e];
     }
     __syncthreads();
     if (tid < BN && n0 + tid < p.N) {
-      float a = 0.f, b = 0.f;
+      float a = 0.f, b = 0.f, d = 0.f;
       for (int r = 0; r < RSTEP; ++r) {
-        a += red[(r * BN + tid) * 2 + 0];
-        b += red[(r * BN + tid) * 2 + 1];
+        a += red[(r * BN + tid) * NS + 0];
+        b += red[(r * BN + tid) * NS + 1];
+        if (two) d += red[(r * BN + tid) * NS + 2];
       }
       const int blk = p.stats_seg_blocks > 0
                           ? seg * p.stats_seg_blocks + p.stats_base + (m0 - seg * p.seg_rows) / BM
                           : mb;
       p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
       p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
+      if (two) {
+        p.stats2[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
+        p.stats2[((size_t)blk * 2 + 1) * p.N + n0 + tid] = d;
+      }
     }
   }
 }
@@ -653,7 +677,7 @@ void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   const int grid = a.nMb * a.nNb;
   size_t lds = (size_t)2 * (BM + BN) * 64 * 2;
   const size_t cst = (size_t)BM * (BN + 8) * 2;
-  const size_t red = (size_t)(256 / (BN / 8)) * BN * 2 * 4;
+  const size_t red = (size_t)(256 / (BN / 8)) * BN * 3 * 4;
   if (cst > lds) lds = cst;
   if (red > lds) lds = red;
   hipLaunchKernelGGL((igemm_nt<BM, BN, WM, WN, PRO, EPI>), dim3(grid), dim3(256), lds, s, a);
@@ -676,7 +700,12 @@ void launch_igemm(const IgemmArgs& a, hipStream_t s) {
     case 1: launch_igemm_t<BM, BN, WM, WN, false, 1>(a, s); break;
     case 2: launch_igemm_t<BM, BN, WM, WN, false, 2>(a, s); break;
     case 3: launch_igemm_t<BM, BN, WM, WN, false, 3>(a, s); break;
-    case 4: launch_igemm_t<BM, BN, WM, WN, false, 4>(a, s); break;
+    case 4:
+      if (a.stats2 != nullptr)
+        launch_igemm_t<BM, BN, WM, WN, false, 5>(a, s);
+      else
+        launch_igemm_t<BM, BN, WM, WN, false, 4>(a, s);
+      break;
     default: launch_igemm_t<BM, BN, WM, WN, false, 0>(a, s); break;
   }
 }
@@ -730,6 +759,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.pro_relu = f.pro_relu;
   a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b; a.epi_c = f.epi_c;
   a.epi_mask = f.epi_mask;
+  a.epi_c2 = f.epi_c2; a.epi_mi2 = f.epi_mi2; a.stats2 = f.stats2;
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);

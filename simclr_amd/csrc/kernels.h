@@ -31,6 +31,9 @@ struct ConvFusion {
   const uint16_t* epi_b = nullptr;
   const uint16_t* epi_c = nullptr;  // mode 4: pre-BN activation for x̂
   const uint8_t* epi_mask = nullptr;  // mode 4: ReLU bitmask of the block input (see bn_apply_ss)
+  const uint16_t* epi_c2 = nullptr;   // mode 4: second x̂ source (producer's downsample BN input)
+  const float* epi_mi2 = nullptr;     //   and its mean/invstd [2][S][N]
+  float* stats2 = nullptr;            //   partials Σg, Σg·x̂2 (layout of stats)
   const float* epi_ss = nullptr;  // mode 3: [2][S][N] scale/shift
   const float* epi_mi = nullptr;  // mode 3/4: [2][S][N] mean/invstd
   int epi_S = 1;
@@ -103,11 +106,18 @@ void bn_bwd_finalize(const float* sums, const float* mean_invstd, const float* g
                      float count, float* dgamma, float* dbeta, float* coef, hipStream_t s);
 void bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef,
                   int R, int C, int S, int relu, uint16_t* dx, uint16_t* dres, hipStream_t s);
+// two BatchNorms fed by the same gradient (residual block: last BN + downsample BN):
+// dx1 = A1·g + B1·x1 + D1, dx2 = A2·g + B2·x2 + D2 in one pass over g
+void bn_bwd_apply2(const uint16_t* g, const uint16_t* x1, const float* coef1, uint16_t* dx1,
+                   const uint16_t* x2, const float* coef2, uint16_t* dx2, int R, int C, int S,
+                   hipStream_t s);
 
 // ---- misc.hip
 void avgpool_fwd(const uint16_t* x, uint16_t* y, int Nb, int HW, int C, hipStream_t s);
 void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int Nb, int HW, int C, hipStream_t s);
-void colsum_bf16(const uint16_t* x, int R, int C, float* out, float beta, hipStream_t s);
+int colsum_groups(int R);  // workspace = colsum_groups(R) * C floats
+void colsum_bf16(const uint16_t* x, int R, int C, float* out, float beta, float* ws,
+                 hipStream_t s);
 void cast_f32_bf16(const float* x, uint16_t* y, size_t n, hipStream_t s);
 void cast_bf16_f32(const uint16_t* x, float* y, size_t n, hipStream_t s);
 

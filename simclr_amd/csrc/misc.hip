@@ -46,21 +46,34 @@ __global__ void k_avgpool_bwd(const uint16_t* __restrict__ dy, uint16_t* __restr
   }
 }
 
-// out[c] = beta*out[c] + Σ_r x[r][c]; block per 64-column strip, threads stride rows
-__global__ void k_colsum(const uint16_t* __restrict__ x, int R, int C, float* __restrict__ out,
-                         float beta) {
+// Column sums in two deterministic levels: grid (C/64 strips, G row groups) writes partials
+// ws[G][C]; k_colsum_final adds the G partials in order.  (One 64-column strip per block over
+// all rows left a 2048-column, 1024-row head-bias gradient latency-bound at ~75 µs.)
+__global__ void k_colsum(const uint16_t* __restrict__ x, int R, int C, float* __restrict__ ws) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;
+  const int G = gridDim.y, g = blockIdx.y;
+  const int per = (R + G - 1) / G;
+  const int r0 = g * per, r1 = min(R, r0 + per);
   float a = 0.f;
   if (c < C)
-    for (int r = rl; r < R; r += 4) a += bf2f(x[(size_t)r * C + c]);
+#pragma unroll 4
+    for (int r = r0 + rl; r < r1; r += 4) a += bf2f(x[(size_t)r * C + c]);
   red[rl][threadIdx.x & 63] = a;
   __syncthreads();
-  if (rl == 0 && c < C) {
-    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    out[c] = beta != 0.f ? beta * out[c] + s : s;
-  }
+  if (rl == 0 && c < C)
+    ws[(size_t)g * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                            red[3][threadIdx.x];
+}
+
+__global__ void k_colsum_final(const float* __restrict__ ws, int G, int C, float* __restrict__ out,
+                               float beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += ws[(size_t)g * C + c];
+  out[c] = beta != 0.f ? beta * out[c] + s : s;
 }
 
 __global__ void k_cast_f32_bf16(const float* __restrict__ x, uint16_t* __restrict__ y, size_t n) {
@@ -96,8 +109,16 @@ void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int Nb, int HW, int C, hipStr
   HIP_CHECK_LAUNCH();
 }
 
-void colsum_bf16(const uint16_t* x, int R, int C, float* out, float beta, hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum, dim3((C + 63) / 64), dim3(256), 0, s, x, R, C, out, beta);
+int colsum_groups(int R) {
+  int g = R / 64;
+  return g < 1 ? 1 : (g > 32 ? 32 : g);
+}
+
+void colsum_bf16(const uint16_t* x, int R, int C, float* out, float beta, float* ws,
+                 hipStream_t s) {
+  const int G = colsum_groups(R);
+  hipLaunchKernelGGL(k_colsum, dim3((C + 63) / 64, G), dim3(256), 0, s, x, R, C, ws);
+  hipLaunchKernelGGL(k_colsum_final, dim3((C + 255) / 256), dim3(256), 0, s, ws, G, C, out, beta);
   HIP_CHECK_LAUNCH();
 }
 

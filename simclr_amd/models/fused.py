@@ -87,6 +87,7 @@ class _ConvSpec:
 class _BlockSpec:
     convs: List[_ConvSpec]
     down: Optional[_ConvSpec]
+    name: str = ""
 
 
 @dataclass
@@ -118,8 +119,8 @@ class FusedStages:
         self.S = segments
         self.calls = 0
         self.blocks: List[_BlockSpec] = []
-        for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4):
-            for blk in layer:
+        for li, layer in enumerate((resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4)):
+            for bi, blk in enumerate(layer):
                 if isinstance(blk, Bottleneck):
                     convs = [_ConvSpec(blk.conv1, blk.bn1, 1, 1, 0),
                              _ConvSpec(blk.conv2, blk.bn2, blk.stride, 3, 1),
@@ -132,7 +133,7 @@ class FusedStages:
                 down = None
                 if blk.downsample is not None:
                     down = _ConvSpec(blk.downsample[0], blk.downsample[1], blk.stride, 1, 0)
-                self.blocks.append(_BlockSpec(convs, down))
+                self.blocks.append(_BlockSpec(convs, down, f"layer{li + 1}.{bi}"))
 
     # ------------------------------------------------------------------ feasibility
     def supported(self, x: torch.Tensor) -> bool:
@@ -273,9 +274,12 @@ class FusedStages:
         ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
         (segment-major across stride-2 parity classes) → (dx, partial, blocks_per_segment):
           ("mask", a_prev, bn_state)      mode 3: g = dx·[bn(a_prev) > 0] (BN+ReLU producer)
-          ("res", resid, mask, a_prev, mi) mode 4: g = (dx + resid)·[y > 0] (residual-block
+          ("res", resid, mask, a_prev, mi, ad, mid)
+                                          mode 4: g = (dx + resid)·[y > 0] (residual-block
                                           producer: mask = its output's ReLU bitmask, a_prev =
-                                          its last pre-BN activation); resid may alias dx
+                                          its last pre-BN activation; resid may alias dx); with
+                                          ``ad`` (the producer's downsample pre-BN activation)
+                                          the partials of its downsample BN too → (p3, pd)
         """
         Nb, H, W, Ci = in_shape
         _, OH, OW, Co = dyn.shape
@@ -328,7 +332,7 @@ class FusedStages:
             epi = (3, None, a_prev)
             tables = (bs.ss.view(-1), bs.mi)
         else:
-            _, resid, mask, a_prev, mi = bn_epi
+            _, resid, mask, a_prev, mi, ad_prev, mid_prev = bn_epi
             epi = (4, resid, None, a_prev, mask)
             tables = (None, mi)
         chosen = []
@@ -339,11 +343,17 @@ class FusedStages:
             chosen.append((wt, g, M, seg, ops.igemm_variant_bm(v), v))
         seg_blocks = sum(seg // bm for (_, _, _, seg, bm, _) in chosen)
         partial = torch.empty((S * seg_blocks * 2 * Ci,), device=dev, dtype=torch.float32)
+        second, partial2 = None, None
+        if bn_epi[0] == "res" and bn_epi[5] is not None:
+            partial2 = torch.empty_like(partial)
+            second = (bn_epi[5], bn_epi[6], partial2)
         base = 0
         for wt, g, M, seg, bm, v in chosen:
             igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
-                         epi_tables=tables, remap=(seg_blocks, base))
+                         epi_tables=tables, remap=(seg_blocks, base), second=second)
             base += seg // bm
+        if partial2 is not None:
+            return dx, (partial, partial2), seg_blocks
         return dx, partial, seg_blocks
 
     # ------------------------------------------------------------------ forward / backward
@@ -358,7 +368,8 @@ class FusedStages:
             tp = _BlockTape(x=x)
             pro_ss = None
             cur = x
-            for cs in b.convs:
+            for ci_, cs in enumerate(b.convs):
+                _ext.TAG = f"{b.name} conv{ci_ + 1} fwd"
                 if pro_ss is not None and cs.k > 1:
                     # a k x k conv re-gathers every input pixel k² times: applying BN+ReLU in
                     # its prologue costs more VALU work than one materialising pass (measured)
@@ -376,18 +387,22 @@ class FusedStages:
             out = torch.empty_like(aL)
             # the next block's input-gradient epilogue only needs [out > 0]: 1 bit per element
             mask = torch.empty((aL.numel() // 8,), device=aL.device, dtype=torch.uint8)
+            _ext.TAG = f"{b.name} ds fwd"
             if b.down is not None:
                 ad, partial, nblk = self._conv_fwd(ops, x, b.down, None, S)
                 rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
                 tp.ad = ad
                 tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st)
+                _ext.TAG = f"{b.name} out fwd"
                 ops.bn_apply_ss(aL, bsL.ss, ad, tp.bnd.ss, out, S, True, mask)
             else:
+                _ext.TAG = f"{b.name} out fwd"
                 ops.bn_apply_ss(aL, bsL.ss, x, None, out, S, True, mask)
             tp.out = out
             tp.mask = mask
             tapes.append(tp)
             x = out
+        _ext.TAG = ""
         return x, tapes
 
     def backward(self, gout: torch.Tensor, tapes: List[_BlockTape]) -> torch.Tensor:
@@ -412,6 +427,7 @@ class FusedStages:
         kernel and finished after it, so its latency hides behind the wgrad."""
         out = tp.out
         L = len(b.convs) - 1
+        _ext.TAG = f"{b.name} bn{L + 1} bwd"
         aL, bsL = tp.acts[L], tp.bns[L]
         C = aL.shape[-1]
         R = aL.numel() // C
@@ -426,46 +442,74 @@ class FusedStages:
             ops.bn_bwd_apply(g, out, aL, coefL, S, True, da, g3)  # g3 = g·[out > 0]
         else:
             g3 = g
-            coefL = self._bn_bwd_finish(ops, pre, S)
-            ops.bn_bwd_apply(g3, None, aL, coefL, S, False, da, None)
+            h3, hd = pre
+            coefL = self._bn_bwd_finish(ops, h3, S)
+            if hd is None:
+                ops.bn_bwd_apply(g3, None, aL, coefL, S, False, da, None)
         dad = None
         if b.down is not None:
-            nblk_d = ops.bn_blocks(R, C, S)
-            partial_d = torch.empty((S * nblk_d * 2 * C,), device=dev, dtype=torch.float32)
-            ops.bn_bwd_reduce(g3, None, tp.ad, tp.bnd.mi, S, False, partial_d)
-            coefd = self._bn_bwd(ops, b.down.bn, partial_d, nblk_d, tp.bnd, S, st)
+            _ext.TAG = f"{b.name} bnds bwd"
             dad = torch.empty_like(tp.ad)
-            ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
+            if pre is not None and hd is not None:
+                # both BNs of the block output from one pass over g3 (their partials came
+                # from the following block's dgrad epilogue)
+                coefd = self._bn_bwd_finish(ops, hd, S)
+                ops.bn_bwd_apply2(g3, aL, coefL, da, tp.ad, coefd, dad, S)
+            else:
+                nblk_d = ops.bn_blocks(R, C, S)
+                partial_d = torch.empty((S * nblk_d * 2 * C,), device=dev, dtype=torch.float32)
+                ops.bn_bwd_reduce(g3, None, tp.ad, tp.bnd.mi, S, False, partial_d)
+                coefd = self._bn_bwd(ops, b.down.bn, partial_d, nblk_d, tp.bnd, S, st)
+                if pre is not None:
+                    ops.bn_bwd_apply2(g3, aL, coefL, da, tp.ad, coefd, dad, S)
+                else:
+                    ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
         # conv chain, last to first: dgrad (+ BN-bwd partials) → start BN all-reduce → wgrad →
         # finish BN → apply
         for i in range(L, 0, -1):
             cs = b.convs[i]
             xin, pro_ss = tp.ins[i]
             a_prev, bs_prev = tp.acts[i - 1], tp.bns[i - 1]
+            _ext.TAG = f"{b.name} conv{i + 1} dgrad"
             gm, part, nb = self._dgrad(ops, da, cs, a_prev.shape, S, bn_epi=("mask", a_prev, bs_prev))
             h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
+            _ext.TAG = f"{b.name} conv{i + 1} wgrad"
             self._wgrad(ops, da, xin, cs, pro_ss, S)
+            _ext.TAG = f"{b.name} bn{i} bwd"
             coef = self._bn_bwd_finish(ops, h, S)
             da_next = torch.empty_like(a_prev)
             ops.bn_bwd_apply(gm, None, a_prev, coef, S, False, da_next, None)
             da = da_next
         cs0 = b.convs[0]
         if b.down is not None:
+            _ext.TAG = f"{b.name} ds dgrad"
             resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
         else:
             resid = g3
+        _ext.TAG = f"{b.name} conv1 dgrad"
         if prev is None:
             dx, _, _ = self._dgrad(ops, da, cs0, tp.x.shape, S, accumulate=True, dx=resid)
             h = None
         else:
             pb, ptp = prev
+            pds = pb.down is not None
             dx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S,
                                        dx=resid if b.down is not None else None,
-                                       bn_epi=("res", resid, ptp.mask, ptp.acts[-1], ptp.bns[-1].mi))
-            h = self._bn_bwd_start(ops, pb.convs[-1].bn, part, nb, ptp.bns[-1], S, st)
+                                       bn_epi=("res", resid, ptp.mask, ptp.acts[-1],
+                                               ptp.bns[-1].mi, ptp.ad if pds else None,
+                                               ptp.bnd.mi if pds else None))
+            if pds:
+                p3, pd = part
+                h = (self._bn_bwd_start(ops, pb.convs[-1].bn, p3, nb, ptp.bns[-1], S, st),
+                     self._bn_bwd_start(ops, pb.down.bn, pd, nb, ptp.bnd, S, st))
+            else:
+                h = (self._bn_bwd_start(ops, pb.convs[-1].bn, part, nb, ptp.bns[-1], S, st), None)
+        _ext.TAG = f"{b.name} conv1 wgrad"
         self._wgrad(ops, da, tp.x, cs0, None, S)
         if b.down is not None:
+            _ext.TAG = f"{b.name} ds wgrad"
             self._wgrad(ops, dad, tp.x, b.down, None, S)
+        _ext.TAG = ""
         return dx, h
 
 

@@ -57,3 +57,8 @@ def require() -> None:
 def ops():
     require()
     return torch.ops.simclr_amd
+
+
+# Semantic label of the op being issued (set by the fused executor, read by profilers such as
+# tools/layer_profile.py); plain attribute, no cost on the hot path.
+TAG = ""

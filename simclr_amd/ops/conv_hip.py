@@ -65,14 +65,16 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
 
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
-                 seg_rows: int = 0, epi_tables=None, remap=(0, 0)) -> None:
+                 seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None) -> None:
+    """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip)."""
     psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
     em = epi[4] if epi is not None and len(epi) > 4 else None
     ess, emi = epi_tables if epi_tables is not None else (None, None)
+    c2, mi2, st2 = second if second is not None else (None, None, None)
     ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-              seg_rows, remap[0], remap[1], ec, em)
+              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2)
 
 
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):

@@ -30,7 +30,9 @@ class _Timed:
             s.record()
             r = f(*args, **kw)
             e.record()
-            self._log.append((_label(name, args), s, e))
+            from simclr_amd.ops import _ext as ext
+            lab, fl = _label(name, args)
+            self._log.append(((lab, fl, ext.TAG), s, e))
             return r
         return wrap
 
@@ -85,11 +87,18 @@ def main():
         tr.step(next(it)[0])
     torch.cuda.synchronize()
     agg = defaultdict(lambda: [0, 0.0, 0.0])
-    for (lab, flops), s, e in log:
+    by_tag = defaultdict(float)
+    for (lab, flops, tag), s, e in log:
         v = agg[lab]
         v[0] += 1
-        v[1] += s.elapsed_time(e) * 1e3
+        t = s.elapsed_time(e) * 1e3
+        v[1] += t
         v[2] += flops
+        # aggregate blocks of the same stage: "layer1.2 conv3 dgrad" -> "layer1 conv3 dgrad"
+        parts = tag.split(" ")
+        if parts and parts[0].startswith("layer"):
+            parts[0] = parts[0].split(".")[0] + (".0" if parts[0].endswith(".0") else ".x")
+        by_tag[" ".join(parts) or "(stem/head/loss/optim)"] += t
     tot = sum(v[1] for v in agg.values()) / a.steps
     print(f"# per-op time, ResNet-50 CIFAR, batch {a.batch}x2 views, avg of {a.steps} steps\n")
     print(f"total timed op time/step: {tot / 1e3:.2f} ms\n")
@@ -97,6 +106,10 @@ def main():
     for lab, (n, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         tf = f"{fl / (t * 1e-6) / 1e12:.0f}" if fl else ""
         print(f"| {lab} | {n / a.steps:.1f} | {t / a.steps:.1f} | {100 * t / a.steps / tot:.1f} | {tf} |")
+    print("\n## by executor stage / op (layerN.0 = first block, layerN.x = the rest)\n")
+    print("| stage op | us/step | % |\n|---|---:|---:|")
+    for k, t in sorted(by_tag.items(), key=lambda kv: -kv[1]):
+        print(f"| {k} | {t / a.steps:.1f} | {100 * t / a.steps / tot:.1f} |")
 
 
 if __name__ == "__main__":
