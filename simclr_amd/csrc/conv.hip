@@ -391,6 +391,15 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
 }
 
 // ------------------------------------------------------------------------------------ wgrad
+// Physical element offset of (row r, element col) in a W-wide swizzled LDS row (see wgrad_tn):
+// 4-element units are XOR-permuted by a row-dependent multiple of 4 units (so 16-byte chunks
+// stay contiguous and in-row).
+template <int W>
+__device__ __forceinline__ int tr_swz(int r, int col) {
+  const int k = W >= 128 ? ((r & 3) | (((r >> 3) & 1) << 2)) : (((r >> 1) & 1) ^ (((r >> 3) & 1) << 1));
+  return ((((col >> 2) ^ (k << 2))) << 2) | (col & 3);
+}
+
 struct WgradArgs {
   const uint16_t* dY;  // [M][N] rows = forward output pixels
   const uint16_t* X;   // forward input NHWC
@@ -410,8 +419,11 @@ template <int BCO, int BKK, int WM, int WN, bool PRO>
 __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn(WgradArgs p) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
   constexpr int FM = TCO / 16, FN = TKK / 16;
-  constexpr int SD = BCO + 8;   // LDS row stride (elements) of the dY tile
-  constexpr int SX = BKK + 8;   // of the X tile
+  // LDS images: unpadded rows with an XOR swizzle of 4-element (8-byte) units per row, chosen so
+  // that every ds_read_b64_tr_b16 half-wave (rows q and q+8, 4 units each) hits 64 distinct
+  // banks (modelled, then SQ_LDS_BANK_CONFLICT: the padded layout measured 0.5 conflicts/access)
+  constexpr int SD = BCO;       // LDS row stride (elements) of the dY tile
+  constexpr int SX = BKK;       // of the X tile
   constexpr int CPD = BCO / 8, CPX = BKK / 8;
   constexpr int DCH = 64 * CPD / 256, XCH = 64 * CPX / 256;
   constexpr int RD = 256 / CPD, RX = 256 / CPX;
@@ -524,14 +536,15 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < DCH; ++j)
-      *(u32x4*)(Ds + buf * 64 * SD + (drow + RD * j) * SD + dch * 8) = rd[j];
+      *(u32x4*)(Ds + buf * 64 * SD + (drow + RD * j) * SD + tr_swz<BCO>(drow + RD * j, dch * 8)) =
+          rd[j];
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       u32x4 v = rx[j];
       if (pro)
         v = xseg[j] ? affine_relu8(v, psc1, psh1, xok[j], p.pro_relu != 0)
                     : affine_relu8(v, psc0, psh0, xok[j], p.pro_relu != 0);
-      *(u32x4*)(Xs + buf * 64 * SX + (xrow + RX * j) * SX + xch * 8) = v;
+      *(u32x4*)(Xs + buf * 64 * SX + (xrow + RX * j) * SX + tr_swz<BKK>(xrow + RX * j, xch * 8)) = v;
     }
   };
 
@@ -559,8 +572,10 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
         const int col = wm * TCO + fm * 16 + 4 * pp;
-        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Db + r1 * SD + col));
-        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Db + (r1 + 4) * SD + col));
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Db + r1 * SD + tr_swz<BCO>(r1, col)));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Db + (r1 + 4) * SD + tr_swz<BCO>(r1 + 4, col)));
         typedef short i16x8 __attribute__((ext_vector_type(8)));
         i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[fm] = __builtin_bit_cast(bf16x8, v);
@@ -568,8 +583,10 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int col = wn * TKK + fn * 16 + 4 * pp;
-        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Xb + r1 * SX + col));
-        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, Xb + (r1 + 4) * SX + col));
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Xb + r1 * SX + tr_swz<BKK>(r1, col)));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Xb + (r1 + 4) * SX + tr_swz<BKK>(r1 + 4, col)));
         typedef short i16x8 __attribute__((ext_vector_type(8)));
         i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[fn] = __builtin_bit_cast(bf16x8, v);
@@ -717,7 +734,7 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   a.nCo = (a.N + BCO - 1) / BCO;
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
-  const size_t lds = (size_t)2 * 64 * ((BCO + 8) + (BKK + 8)) * 2;
+  const size_t lds = (size_t)2 * 64 * (BCO + BKK) * 2;
   if (pro)
     hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true>), dim3(grid), dim3(256), lds, s, a);
   else
