@@ -106,6 +106,19 @@ def main():
     for lab, (n, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         tf = f"{fl / (t * 1e-6) / 1e12:.0f}" if fl else ""
         print(f"| {lab} | {n / a.steps:.1f} | {t / a.steps:.1f} | {100 * t / a.steps / tot:.1f} | {tf} |")
+    from simclr_amd.ops import tuning
+    print("\n## autotuned tile variants (key -> variant)\n")
+    ops = real
+    for key, v in sorted(tuning.table().items(), key=lambda kv: str(kv[0])):
+        if key[0] == "igemm":
+            g = key[1]
+            desc = f"M={g[0] * g[4] * g[5]} N={g[14]} K={g[6] * g[7] * g[3]} epi{key[4]}{' pro' if key[3] else ''}"
+            tile = f"{ops.igemm_variant_bm(v)}x{ops.igemm_variant_bn(v)}"
+        else:
+            g = key[1]
+            desc = f"wgrad M={g[0] * g[4] * g[5]} N={g[14]} K={g[6] * g[7] * g[3]}{' pro' if key[3] else ''}"
+            tile = f"v{v}"
+        print(f"- {key[0]} {desc}: {tile}")
     print("\n## by executor stage / op (layerN.0 = first block, layerN.x = the rest)\n")
     print("| stage op | us/step | % |\n|---|---:|---:|")
     for k, t in sorted(by_tag.items(), key=lambda kv: -kv[1]):
