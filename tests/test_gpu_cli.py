@@ -1,0 +1,70 @@
+"""End-to-end CLI on the MI355X fast path: pretrain ResNet-50 (CIFAR stem) through the fused
+stage executor with the step captured in a hipGraph → reference-format checkpoint → eval
+(centroid, linear probe on the GPU) → resume, and the supervised baseline (single-segment
+executor).  Synthetic data (no network on the box)."""
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+COMMON = ["data.synthetic=true", "data.synthetic_size=512", "experiment.batches=64",
+          "experiment.base_cnn=resnet50", "model.cifar_stem=true"]
+
+
+def _run(script, args, cwd):
+    r = subprocess.run([sys.executable, str(ROOT / script), *args], cwd=str(cwd),
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout + r.stderr
+
+
+@pytest.mark.timeout(1200)
+def test_gpu_pretrain_graph_eval_resume(tmp_path):
+    run = tmp_path / "run"
+    out = _run("main.py", COMMON + ["parameter.epochs=2", "parameter.warmup_epochs=1",
+                                    "experiment.save_model_epoch=1", "runtime.hip_graph=true",
+                                    f"hydra.run.dir={run}"], tmp_path)
+    assert "Epoch:2/2 progress:1.000 loss:" in out
+    loss = float([l for l in out.splitlines() if "Epoch:2/2" in l][0].split("loss:")[1].split(",")[0])
+    assert loss == loss and 0.0 < loss < 20.0
+    ck = torch.load(run / "epoch=2-cifar10.pt", weights_only=True)
+    assert all(k.startswith("module.") for k in ck)
+    assert ck["module.f.conv1.weight"].shape == (64, 3, 3, 3)
+    assert ck["module.f.conv1.weight"].dtype == torch.float32
+    assert all(torch.isfinite(v.float()).all() for v in ck.values())
+    # resume from epoch 1 (eager, no graph) reproduces epoch 2's loss closely
+    run2 = tmp_path / "run2"
+    out2 = _run("main.py", COMMON + ["parameter.epochs=2", "parameter.warmup_epochs=1",
+                                     "experiment.save_model_epoch=1", f"hydra.run.dir={run2}",
+                                     f"runtime.resume={run / 'resume-1.pt'}"], tmp_path)
+    l2 = float([l for l in out2.splitlines() if "Epoch:2/2" in l][0].split("loss:")[1].split(",")[0])
+    assert abs(l2 - loss) < 0.05, (loss, l2)
+    ev = tmp_path / "ev"
+    _run("eval.py", ["data.synthetic=true", "data.synthetic_size=512", "experiment.batches=64",
+                     "experiment.base_cnn=resnet50", "model.cifar_stem=true",
+                     f"experiment.target_dir={run}", f"hydra.run.dir={ev}"], tmp_path)
+    res = json.loads((ev / "results.json").read_text())
+    assert set(res) == {"epoch=1-cifar10.pt", "epoch=2-cifar10.pt"}
+    assert 0.0 <= res["epoch=2-cifar10.pt"]["val_acc"] <= 1.0
+    ev2 = tmp_path / "ev2"
+    _run("eval.py", ["data.synthetic=true", "data.synthetic_size=512", "experiment.batches=64",
+                     "experiment.base_cnn=resnet50", "model.cifar_stem=true",
+                     f"experiment.target_dir={run}", "parameter.classifier=linear",
+                     "parameter.epochs=2", f"hydra.run.dir={ev2}"], tmp_path)
+    r2 = json.loads((ev2 / "results.json").read_text())["epoch=2-cifar10.pt"]
+    assert len(r2["val_accuracies"]) == 2
+
+
+@pytest.mark.timeout(900)
+def test_gpu_supervised(tmp_path):
+    run = tmp_path / "sup"
+    out = _run("supervised.py", COMMON + ["parameter.epochs=2", "parameter.warmup_epochs=1",
+                                          f"hydra.run.dir={run}"], tmp_path)
+    assert "val acc:" in out
+    assert len(list(run.glob("epoch=*-cifar10.pt"))) == 1
