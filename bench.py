@@ -120,7 +120,8 @@ def run_reference(args, rank, world, dev):
     from bench.torch_reference import (PlainContrastive, exclude_from_wt_decay, larc_step,
                                        nt_xent_reference)
     torch.manual_seed(7)
-    model = PlainContrastive(args.model, stem="cifar" if args.cifar_stem else "imagenet").to(dev)
+    ref_stem = "reference_cifar" if args.model == "resnet18" else "imagenet"
+    model = PlainContrastive(args.model, stem="cifar" if args.cifar_stem else ref_stem).to(dev)
     if world > 1:
         model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
@@ -149,14 +150,31 @@ def run_reference(args, rank, world, dev):
     return time.perf_counter() - t0, float(loss.item())
 
 
+def _stem_key(args) -> str:
+    if args.cifar_stem:
+        return "cifar"
+    return "refstem" if args.model == "resnet18" else "imagenet"
+
+
+def _stem_label(args) -> str:
+    if args.cifar_stem:
+        return "cifar-stem"
+    return ("reference-stem(3x3/p3)" if args.model == "resnet18"
+            else "imagenet-stem(7x7/s2+maxpool)")
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--cifar-stem", dest="cifar_stem", action="store_true", default=True)
-    ap.add_argument("--imagenet-stem", dest="cifar_stem", action="store_false")
+    ap.add_argument("--cifar-stem", dest="cifar_stem", action="store_true", default=True,
+                    help="3x3/s1/p1 stem, no maxpool (the north star's CIFAR-ResNet; default)")
+    ap.add_argument("--reference-stem", "--imagenet-stem", dest="cifar_stem",
+                    action="store_false",
+                    help="the stem the reference builds: r50 ImageNet 7x7/s2 + maxpool, "
+                         "r18 3x3/s1/p3 (model.py:90-104)")
     ap.add_argument("--batch", type=int, default=512, help="images per GPU")
     ap.add_argument("--size", type=int, default=32)
     ap.add_argument("--precision", default="bf16")
@@ -185,7 +203,7 @@ def main(argv=None):
     if bpath.exists():
         try:
             b = json.loads(bpath.read_text())
-            key = f"{args.model}-{'cifar' if args.cifar_stem else 'imagenet'}-b{args.batch}"
+            key = f"{args.model}-{_stem_key(args)}-b{args.batch}"
             per_gpu = b.get("images_per_sec_per_gpu", {}).get(key)
             if per_gpu:
                 base = per_gpu * world
@@ -206,8 +224,9 @@ def main(argv=None):
         "data": "synthetic 32x32 uint8 CIFAR-shape images, random-init weights, on-device "
                 "SimCLR augmentation",
         "config": {
-            "model": f"{args.model}-{'cifar-stem' if args.cifar_stem else 'imagenet-stem'}"
-                     "+projection-head(2048-2048-128)",
+            "model": f"{args.model}-{_stem_label(args)}"
+                     f"+projection-head({2048 if args.model == 'resnet50' else 512}-"
+                     f"{2048 if args.model == 'resnet50' else 512}-128)",
             "global_batch": args.batch * world,
             "per_gpu_batch": args.batch,
             "views": 2,
