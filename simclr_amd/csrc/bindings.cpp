@@ -104,7 +104,8 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const c10::optional<Tensor>& epi_mi, int64_t seg_rows, int64_t stats_seg_blocks,
            int64_t stats_base, const c10::optional<Tensor>& epi_c,
            const c10::optional<Tensor>& epi_mask, const c10::optional<Tensor>& epi_c2,
-           const c10::optional<Tensor>& epi_mi2, const c10::optional<Tensor>& stats2) {
+           const c10::optional<Tensor>& epi_mi2, const c10::optional<Tensor>& stats2,
+           const c10::optional<Tensor>& pro_d, const c10::optional<Tensor>& A2) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -171,6 +172,14 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
                 "igemm prologue: segment rows must be a multiple of the tile rows");
     TORCH_CHECK(pro_sc->numel() >= (M / pro_seg_rows) * g.C, "igemm prologue: [S][C] size");
   }
+  if (pro_d.has_value() && pro_d->defined()) {
+    TORCH_CHECK(f.pro_sc, "igemm BN-backward prologue needs pro_sc (A) and pro_sh (B)");
+    TORCH_CHECK(pro_d->numel() >= (M / pro_seg_rows) * g.C, "igemm prologue: d [S][C] size");
+    TORCH_CHECK(A2.has_value() && A2->numel() == A.numel(), "igemm prologue: A2 must match A");
+    TORCH_CHECK(epi_mode == 0 || epi_mode == 3, "igemm BN-backward prologue: epilogue 0 or 3");
+    f.pro_d = f32(*pro_d, "pro_d");
+    f.A2 = bf(*A2, "A2");
+  }
   conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
                 optf32w(stats, "stats"), f, (int)variant, cur_stream());
 }
@@ -188,7 +197,9 @@ int64_t wgrad_nsplit(std::vector<int64_t> gv, int64_t variant) {
 void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tensor& out,
            std::vector<int64_t> gv, int64_t splits, int64_t creal, double beta,
            const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
-           int64_t pro_seg_rows, bool pro_relu, int64_t pro_S, int64_t variant) {
+           int64_t pro_seg_rows, bool pro_relu, int64_t pro_S, int64_t variant,
+           const c10::optional<Tensor>& dY2, const c10::optional<Tensor>& dp_coef,
+           int64_t dp_seg_rows, int64_t dp_S) {
   const ConvGeom g = geom_from(gv);
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int64_t K = (int64_t)g.KH * g.KW * g.C;
@@ -203,6 +214,19 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
   if (f.pro_sc) {
     // the prologue is indexed by *input* rows, which equal output rows only for 1x1/stride-1
     TORCH_CHECK(pro_seg_rows > 0 && (int64_t)g.Nb % pro_S == 0, "wgrad prologue geometry");
+  }
+  if (dY2.has_value() && dY2->defined()) {
+    TORCH_CHECK(dY2->numel() == dY.numel(), "wgrad: dY2 must match dY");
+    TORCH_CHECK(dp_coef.has_value() && dp_coef->numel() >= 3 * dp_S * g.N, "wgrad: dp_coef [3][S][N]");
+    const int64_t iters = (M + 63) / 64;
+    const int64_t ips = (iters + splits - 1) / splits;
+    TORCH_CHECK(dp_seg_rows > 0 && M % dp_seg_rows == 0 && dp_seg_rows % (ips * 64) == 0 &&
+                    M / dp_seg_rows == dp_S,
+                "wgrad dY prologue: every split must lie inside one segment");
+    f.dY2 = bf(*dY2, "dY2");
+    f.dp_coef = f32(*dp_coef, "dp_coef");
+    f.dp_seg_rows = (int)dp_seg_rows;
+    f.dp_S = (int)dp_S;
   }
   conv_wgrad(g, bf(dY, "dY"), bf(X, "X"), (size_t)X.numel(), f32w(partial, "partial"), (int)splits,
              f32w(out, "out"), (int)creal, (float)beta, f, (int)variant, cur_stream());
@@ -571,14 +595,14 @@ void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int6
 }  // namespace
 
 TORCH_LIBRARY(simclr_amd, m) {
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None) -> ()", &igemm);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
   m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);
   m.def("igemm_variant_bn(int v) -> int", &igemm_vbn);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
-  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1) -> ()", &wgrad);
+  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);
   m.def("bn_blocks(int R, int C, int S) -> int", &bn_blocks);
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);

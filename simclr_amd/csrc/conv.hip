@@ -44,8 +44,12 @@ struct IgemmArgs {
   uint32_t a_bytes, b_bytes;
   int nMb, nNb;
   // prologue (A operand): a = relu?(x * sc[seg][c] + sh[seg][c]); seg = m / pro_seg_rows
+  // or (pro_d != nullptr) the BatchNorm-backward form a = sc·A + sh·A2 + d (da = A·g + B·x + D
+  // of the BN that follows this conv's input in forward order), reading A2 at A's offsets
   const float* pro_sc;
   const float* pro_sh;
+  const float* pro_d;
+  const uint16_t* A2;
   int pro_seg_rows, pro_relu;
   // epilogue: 0 store, 1 out = acc + epi_a, 2 out = acc + (epi_b > 0 ? epi_a : 0),
   // 3 out = g = (epi_b*sc + sh > 0) ? acc : 0 with BatchNorm-backward partials Σg, Σg·x̂
@@ -86,7 +90,20 @@ __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const fl
   return w;
 }
 
-template <int BM, int BN, int WM, int WN, bool PRO, int EPI>
+__device__ __forceinline__ u32x4 bnbwd8(u32x4 g, u32x4 x, const float* A, const float* B,
+                                        const float* D, bool ok) {
+  u32x4 w;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = A[2 * e] * lo_bf(g[e]) + B[2 * e] * lo_bf(x[e]) + D[2 * e];
+    const float b = A[2 * e + 1] * hi_bf(g[e]) + B[2 * e + 1] * hi_bf(x[e]) + D[2 * e + 1];
+    w[e] = ok ? pack2bf(a, b) : 0u;
+  }
+  return w;
+}
+
+// PRO: 0 none, 1 BN-apply + ReLU prologue, 2 BN-backward prologue (two operands)
+template <int BM, int BN, int WM, int WN, int PRO, int EPI>
 __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(IgemmArgs p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -134,11 +151,14 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
     b_off[j] = nrow * p.K;
   }
 
-  u32x4 ra[ACH], rb[BCH];
+  u32x4 ra[ACH], rb[BCH], ra2[ACH];
   bool rok[ACH];
-  float psc[8], psh[8];
-  constexpr bool pro = PRO;
-  const int pseg = pro ? m0 / p.pro_seg_rows : 0;  // block-uniform (host guarantees)
+  float psc[8], psh[8], pdd[8];
+  constexpr bool pro = PRO == 1;
+  constexpr bool bnb = PRO == 2;
+  const int pseg = (pro || bnb) ? m0 / p.pro_seg_rows : 0;  // block-uniform (host guarantees)
+  const __amdgpu_buffer_rsrc_t ra2_src = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(bnb ? p.A2 : p.A), (short)0, (int)p.a_bytes, 0x00020000);
   const uint32_t OOB_A = p.a_bytes, OOB_B = p.b_bytes;
 
   auto gload = [&](int kt) {
@@ -156,8 +176,9 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
       rok[j] = ok;
       const uint32_t off = ok ? (uint32_t)((((a_n[j] * p.IH + ih) * p.IW + iw) * p.C + ci) * 2) : OOB_A;
       ra[j] = __builtin_amdgcn_raw_buffer_load_b128(ra_src, off, 0, 0);
+      if (bnb) ra2[j] = __builtin_amdgcn_raw_buffer_load_b128(ra2_src, off, 0, 0);
     }
-    if (pro) {
+    if (pro || bnb) {
       const int cc = kok ? ci : 0;
       const float4* ps = (const float4*)(p.pro_sc + pseg * p.C + cc);
       const float4* ph = (const float4*)(p.pro_sh + pseg * p.C + cc);
@@ -166,6 +187,12 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
       psc[4] = s1.x; psc[5] = s1.y; psc[6] = s1.z; psc[7] = s1.w;
       psh[0] = h0.x; psh[1] = h0.y; psh[2] = h0.z; psh[3] = h0.w;
       psh[4] = h1.x; psh[5] = h1.y; psh[6] = h1.z; psh[7] = h1.w;
+      if (bnb) {
+        const float4* pq = (const float4*)(p.pro_d + pseg * p.C + cc);
+        const float4 d0 = pq[0], d1 = pq[1];
+        pdd[0] = d0.x; pdd[1] = d0.y; pdd[2] = d0.z; pdd[3] = d0.w;
+        pdd[4] = d1.x; pdd[5] = d1.y; pdd[6] = d1.z; pdd[7] = d1.w;
+      }
     }
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
@@ -178,7 +205,9 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
     for (int j = 0; j < ACH; ++j) {
       const int row = rbase + 32 * j;
       const int ch = cch ^ (row & 7);
-      const u32x4 v = pro ? affine_relu8(ra[j], psc, psh, rok[j], p.pro_relu != 0) : ra[j];
+      const u32x4 v = pro   ? affine_relu8(ra[j], psc, psh, rok[j], p.pro_relu != 0)
+                      : bnb ? bnbwd8(ra[j], ra2[j], psc, psh, pdd, rok[j])
+                            : ra[j];
       *(u32x4*)(As + buf * BM * 64 + row * 64 + ch * 8) = v;
     }
 #pragma unroll
@@ -413,9 +442,14 @@ struct WgradArgs {
   const float* pro_sc;  // X-operand prologue, [S<=2][C]
   const float* pro_sh;
   int pro_seg_rows, pro_relu, pro_S;
+  // dY-operand BatchNorm-backward prologue: dY = A·dY + B·dY2 + D with coef [3][S][N]; every
+  // split lies inside one segment of dp_seg_rows rows (host-aligned)
+  const uint16_t* dY2;
+  const float* dp_coef;
+  int dp_seg_rows, dp_S;
 };
 
-template <int BCO, int BKK, int WM, int WN, bool PRO>
+template <int BCO, int BKK, int WM, int WN, bool PRO, bool DPRO>
 __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn(WgradArgs p) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
   constexpr int FM = TCO / 16, FN = TKK / 16;
@@ -459,7 +493,21 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
   const int kw = tap - kh * p.KW;
   const int OHW = p.OH * p.OW;
 
-  u32x4 rd[DCH], rx[XCH];
+  u32x4 rd[DCH], rx[XCH], rd2[DCH];
+  bool dok[DCH];
+  float dA[8], dB[8], dD[8];
+  const __amdgpu_buffer_rsrc_t rd2_src = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(DPRO ? p.dY2 : p.dY), (short)0, (int)p.dy_bytes, 0x00020000);
+  if (DPRO) {
+    const int dseg = (split * p.iters_per_split * 64) / p.dp_seg_rows;
+    const int cc = dcol_ok ? dcol : 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dA[e] = p.dp_coef[dseg * p.N + cc + e];
+      dB[e] = p.dp_coef[(p.dp_S + dseg) * p.N + cc + e];
+      dD[e] = p.dp_coef[(2 * p.dp_S + dseg) * p.N + cc + e];
+    }
+  }
   bool xok[XCH];
   bool xseg[XCH];
   constexpr bool pro = PRO;
@@ -508,6 +556,10 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
       const int m = mb + drow + RD * j;
       const bool ok = m < mend && dcol_ok;
       rd[j] = __builtin_amdgcn_raw_buffer_load_b128(rd_src, ok ? doff[j] : p.dy_bytes, 0, 0);
+      if (DPRO) {
+        rd2[j] = __builtin_amdgcn_raw_buffer_load_b128(rd2_src, ok ? doff[j] : p.dy_bytes, 0, 0);
+        dok[j] = ok;
+      }
       doff[j] += dstep;
     }
 #pragma unroll
@@ -537,7 +589,7 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 #pragma unroll
     for (int j = 0; j < DCH; ++j)
       *(u32x4*)(Ds + buf * 64 * SD + (drow + RD * j) * SD + tr_swz<BCO>(drow + RD * j, dch * 8)) =
-          rd[j];
+          DPRO ? bnbwd8(rd[j], rd2[j], dA, dB, dD, dok[j]) : rd[j];
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       u32x4 v = rx[j];
@@ -686,7 +738,7 @@ __global__ void weight_transform(const uint16_t* __restrict__ W, uint16_t* __res
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool PRO, int EPI>
+template <int BM, int BN, int WM, int WN, int PRO, int EPI>
 void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   IgemmArgs a = a0;
   a.nMb = (a.M + BM - 1) / BM;
@@ -704,41 +756,53 @@ void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
 // compile-time fusion modes (prologue x epilogue), so each launch carries only its own work
 template <int BM, int BN, int WM, int WN>
 void launch_igemm(const IgemmArgs& a, hipStream_t s) {
+  if (a.pro_d != nullptr) {  // BN-backward prologue: only with a plain or mode-3 epilogue
+    if (a.epi_mode == 3)
+      launch_igemm_t<BM, BN, WM, WN, 2, 3>(a, s);
+    else
+      launch_igemm_t<BM, BN, WM, WN, 2, 0>(a, s);
+    return;
+  }
   if (a.pro_sc != nullptr) {
     switch (a.epi_mode) {
-      case 1: launch_igemm_t<BM, BN, WM, WN, true, 1>(a, s); break;
-      case 2: launch_igemm_t<BM, BN, WM, WN, true, 2>(a, s); break;
-      case 3: launch_igemm_t<BM, BN, WM, WN, true, 3>(a, s); break;
-      default: launch_igemm_t<BM, BN, WM, WN, true, 0>(a, s); break;
+      case 1: launch_igemm_t<BM, BN, WM, WN, 1, 1>(a, s); break;
+      case 2: launch_igemm_t<BM, BN, WM, WN, 1, 2>(a, s); break;
+      case 3: launch_igemm_t<BM, BN, WM, WN, 1, 3>(a, s); break;
+      default: launch_igemm_t<BM, BN, WM, WN, 1, 0>(a, s); break;
     }
     return;
   }
   switch (a.epi_mode) {
-    case 1: launch_igemm_t<BM, BN, WM, WN, false, 1>(a, s); break;
-    case 2: launch_igemm_t<BM, BN, WM, WN, false, 2>(a, s); break;
-    case 3: launch_igemm_t<BM, BN, WM, WN, false, 3>(a, s); break;
+    case 1: launch_igemm_t<BM, BN, WM, WN, 0, 1>(a, s); break;
+    case 2: launch_igemm_t<BM, BN, WM, WN, 0, 2>(a, s); break;
+    case 3: launch_igemm_t<BM, BN, WM, WN, 0, 3>(a, s); break;
     case 4:
       if (a.stats2 != nullptr)
-        launch_igemm_t<BM, BN, WM, WN, false, 5>(a, s);
+        launch_igemm_t<BM, BN, WM, WN, 0, 5>(a, s);
       else
-        launch_igemm_t<BM, BN, WM, WN, false, 4>(a, s);
+        launch_igemm_t<BM, BN, WM, WN, 0, 4>(a, s);
       break;
-    default: launch_igemm_t<BM, BN, WM, WN, false, 0>(a, s); break;
+    default: launch_igemm_t<BM, BN, WM, WN, 0, 0>(a, s); break;
   }
 }
 
 template <int BCO, int BKK, int WM, int WN>
 void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   const bool pro = a0.pro_sc != nullptr;
+  const bool dpro = a0.dY2 != nullptr;
   WgradArgs a = a0;
   a.nCo = (a.N + BCO - 1) / BCO;
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
   const size_t lds = (size_t)2 * 64 * (BCO + BKK) * 2;
-  if (pro)
-    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true>), dim3(grid), dim3(256), lds, s, a);
+  if (pro && dpro)
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true, true>), dim3(grid), dim3(256), lds, s, a);
+  else if (pro)
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true, false>), dim3(grid), dim3(256), lds, s, a);
+  else if (dpro)
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false, true>), dim3(grid), dim3(256), lds, s, a);
   else
-    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false>), dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false, false>), dim3(grid), dim3(256), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -774,6 +838,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.b_bytes = (uint32_t)((size_t)a.N * a.K * 2);
   a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh; a.pro_seg_rows = f.pro_seg_rows > 0 ? f.pro_seg_rows : a.M;
   a.pro_relu = f.pro_relu;
+  a.pro_d = f.pro_d; a.A2 = f.A2;
   a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b; a.epi_c = f.epi_c;
   a.epi_mask = f.epi_mask;
   a.epi_c2 = f.epi_c2; a.epi_mi2 = f.epi_mi2; a.stats2 = f.stats2;
@@ -826,6 +891,8 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh;
   a.pro_seg_rows = f.pro_seg_rows > 0 ? f.pro_seg_rows : a.M;
   a.pro_relu = f.pro_relu; a.pro_S = f.pro_S > 0 ? f.pro_S : 1;
+  a.dY2 = f.dY2; a.dp_coef = f.dp_coef; a.dp_seg_rows = f.dp_seg_rows > 0 ? f.dp_seg_rows : a.M;
+  a.dp_S = f.dp_S > 0 ? f.dp_S : 1;
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
   switch (variant) {
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;

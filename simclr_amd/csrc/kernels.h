@@ -24,6 +24,11 @@ struct ConvFusion {
   int pro_seg_rows = 0;           // rows per segment (BM must divide it for igemm)
   int pro_relu = 0;
   int pro_S = 1;
+  const float* pro_d = nullptr;   // igemm BN-backward prologue: a = sc·A + sh·A2 + d
+  const uint16_t* A2 = nullptr;   //   second A-operand tensor (same geometry as A)
+  const uint16_t* dY2 = nullptr;  // wgrad dY-operand BN-backward prologue (coef [3][S][N])
+  const float* dp_coef = nullptr;
+  int dp_seg_rows = 0, dp_S = 1;
   int epi_mode = 0;               // igemm: 1 out = acc + a; 2 out = acc + (b > 0 ? a : 0);
                                   // 3 out = (b*sc+sh > 0 ? acc : 0) + BN-bwd partials
                                   // 4 out = (b > 0 ? acc + a : 0) + BN-bwd partials vs c

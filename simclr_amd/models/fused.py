@@ -34,6 +34,7 @@ they are final (overlap with the rest of the backward).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
@@ -118,6 +119,8 @@ class FusedStages:
         self.resnet = resnet
         self.S = segments
         self.calls = 0
+        # BN backward of a bottleneck's conv3 inside conv3's dgrad/wgrad operand prologues
+        self.bnb_prologue = os.environ.get("SIMCLR_BNB_PROLOGUE", "1") != "0"
         self.blocks: List[_BlockSpec] = []
         for li, layer in enumerate((resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4)):
             for bi, blk in enumerate(layer):
@@ -256,7 +259,10 @@ class FusedStages:
         return self._bn_bwd_finish(ops, self._bn_bwd_start(ops, bn, partial, nblk_seg, bs, S, st),
                                    S)
 
-    def _wgrad(self, ops, dyn, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int):
+    def _wgrad(self, ops, dyn, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int,
+               bnb: Optional[Tuple] = None):
+        """``bnb = (a, coef)``: dy = coef.A·dyn + coef.B·a + coef.D, the BatchNorm backward of
+        the conv's own BN, computed in the dY operand's prologue (never written to HBM)."""
         Nb, H, W, C = xn.shape
         Co = cs.conv.out_channels
         OH, OW = dyn.shape[1], dyn.shape[2]
@@ -265,10 +271,20 @@ class FusedStages:
         pro = None
         if pro_ss is not None:
             pro = (pro_ss[0], pro_ss[1], M // S, True, S)
-        _deliver_grad(cs.conv.weight, lambda out: run_wgrad(ops, dyn, xn, out, g, C, pro=pro))
+        dpro = (bnb[0], bnb[1], M // S, S) if bnb is not None else None
+        _deliver_grad(cs.conv.weight,
+                      lambda out: run_wgrad(ops, dyn, xn, out, g, C, pro=pro, dpro=dpro))
+
+    def _bnb_ok(self, cs: _ConvSpec, a: torch.Tensor, S: int) -> bool:
+        """The BN-backward operand prologue applies to a 1x1 stride-1 conv whose per-segment
+        rows tile evenly (64-row wgrad splits, 64..256-row dgrad tiles)."""
+        M = a.numel() // a.shape[-1]
+        return (self.bnb_prologue and cs.k == 1 and cs.stride == 1 and M % S == 0
+                and (M // S) % 256 == 0)
 
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
-               dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None):
+               dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,
+               bnb: Optional[Tuple] = None):
         """dx (NHWC) = conv-transpose(dy).  ``accumulate``: dx += result (dx must be given).
 
         ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
@@ -280,6 +296,8 @@ class FusedStages:
                                           its last pre-BN activation; resid may alias dx); with
                                           ``ad`` (the producer's downsample pre-BN activation)
                                           the partials of its downsample BN too → (p3, pd)
+        ``bnb = (a, coef)`` (1x1 stride-1 only): the A operand is the BatchNorm backward
+        coef.A·dyn + coef.B·a + coef.D computed in the prologue.
         """
         Nb, H, W, Ci = in_shape
         _, OH, OW, Co = dyn.shape
@@ -336,10 +354,16 @@ class FusedStages:
             epi = (4, resid, None, a_prev, mask)
             tables = (None, mi)
         chosen = []
+        bpro = None
+        if bnb is not None:
+            assert cs.stride == 1 and cs.k == 1 and len(launches) == 1
+            SC = S * dyn.shape[-1]
+            c = bnb[1]
+            bpro = (c[:SC], c[SC:2 * SC], c[2 * SC:], launches[0][2] // S, bnb[0])
         for wt, g, M in launches:
             seg = M // S
             v = igemm_choose(ops, dyn, wt, dx, g, want_stats=True, epi=epi, seg_rows=seg,
-                             epi_tables=tables)
+                             epi_tables=tables, bnb=bpro)
             chosen.append((wt, g, M, seg, ops.igemm_variant_bm(v), v))
         seg_blocks = sum(seg // bm for (_, _, _, seg, bm, _) in chosen)
         partial = torch.empty((S * seg_blocks * 2 * Ci,), device=dev, dtype=torch.float32)
@@ -350,7 +374,7 @@ class FusedStages:
         base = 0
         for wt, g, M, seg, bm, v in chosen:
             igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
-                         epi_tables=tables, remap=(seg_blocks, base), second=second)
+                         epi_tables=tables, remap=(seg_blocks, base), second=second, bnb=bpro)
             base += seg // bm
         if partial2 is not None:
             return dx, (partial, partial2), seg_blocks
@@ -433,6 +457,7 @@ class FusedStages:
         R = aL.numel() // C
         dev = aL.device
         da = torch.empty_like(aL)
+        lazy = None
         if pre is None:
             nblk = ops.bn_blocks(R, C, S)
             partial = torch.empty((S * nblk * 2 * C,), device=dev, dtype=torch.float32)
@@ -445,7 +470,10 @@ class FusedStages:
             h3, hd = pre
             coefL = self._bn_bwd_finish(ops, h3, S)
             if hd is None:
-                ops.bn_bwd_apply(g3, None, aL, coefL, S, False, da, None)
+                if L > 0 and self._bnb_ok(b.convs[L], aL, S):
+                    lazy = (aL, coefL)  # da never materialised: conv L's operand prologues
+                else:
+                    ops.bn_bwd_apply(g3, None, aL, coefL, S, False, da, None)
         dad = None
         if b.down is not None:
             _ext.TAG = f"{b.name} bnds bwd"
@@ -471,10 +499,12 @@ class FusedStages:
             xin, pro_ss = tp.ins[i]
             a_prev, bs_prev = tp.acts[i - 1], tp.bns[i - 1]
             _ext.TAG = f"{b.name} conv{i + 1} dgrad"
-            gm, part, nb = self._dgrad(ops, da, cs, a_prev.shape, S, bn_epi=("mask", a_prev, bs_prev))
+            dyn, bnb = (g3, lazy) if (i == L and lazy is not None) else (da, None)
+            gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,
+                                       bn_epi=("mask", a_prev, bs_prev), bnb=bnb)
             h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
             _ext.TAG = f"{b.name} conv{i + 1} wgrad"
-            self._wgrad(ops, da, xin, cs, pro_ss, S)
+            self._wgrad(ops, dyn, xin, cs, pro_ss, S, bnb=bnb)
             _ext.TAG = f"{b.name} bn{i} bwd"
             coef = self._bn_bwd_finish(ops, h, S)
             da_next = torch.empty_like(a_prev)

@@ -25,13 +25,16 @@ from . import _ext, tuning
 
 
 def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None,
-                 seg_rows: int = 0, epi_tables=None) -> int:
+                 seg_rows: int = 0, epi_tables=None, bnb=None) -> int:
     """Autotuned tile variant for this problem (admissible: BM divides the segment rows /
     M whenever per-segment prologue, statistics or the mode-3 epilogue need block-uniform
     segments)."""
     M = geom[0] * geom[4] * geom[5]
     N = geom[14]
     psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
+    pd, A2 = None, None
+    if bnb is not None:  # BN-backward prologue: a = coefA·A + coefB·A2 + coefD
+        psc, psh, pd, pseg, A2 = bnb
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     cands = []
@@ -50,7 +53,8 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
     default = 1 if N <= 64 else 0
     if default not in cands:
         default = cands[0]
-    key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows)
+    key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows,
+           bnb is not None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
     em = epi[4] if epi is not None and len(epi) > 4 else None
 
@@ -59,22 +63,27 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
         st = (torch.empty(((M + bm - 1) // bm) * 2 * N, device=out.device, dtype=torch.float32)
               if want_stats else None)
         ops.igemm(A, B, torch.empty_like(out), bias, st, geom, psc, psh, pseg, prelu, emode, ea,
-                  eb, v, ess, emi, seg_rows, 0, 0, ec, em)
+                  eb, v, ess, emi, seg_rows, 0, 0, ec, em, None, None, None, pd, A2)
 
     return tuning.pick(key, cands, default, trial)
 
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
-                 seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None) -> None:
-    """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip)."""
+                 seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None,
+                 bnb=None) -> None:
+    """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip);
+    ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue."""
     psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
+    pd, A2 = None, None
+    if bnb is not None:
+        psc, psh, pd, pseg, A2 = bnb
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
     em = epi[4] if epi is not None and len(epi) > 4 else None
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     c2, mi2, st2 = second if second is not None else (None, None, None)
     ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2)
+              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2)
 
 
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):
@@ -99,17 +108,33 @@ def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=N
     return (stats, M // bm) if stats is not None else None
 
 
-def run_wgrad(ops, dY, X, out, geom, creal, pro=None):
-    """Split-M weight gradient (fp32, written to ``out`` = OHWI) with the autotuned variant."""
+def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
+    """Split-M weight gradient (fp32, written to ``out`` = OHWI) with the autotuned variant.
+
+    ``dpro = (dY2, coef[3][S][N], seg_rows, S)``: the dY operand is the BatchNorm backward
+    A·dY + B·dY2 + D computed on the fly (splits are aligned to the segments)."""
     psc, psh, seg_rows, prelu, pS = pro if pro is not None else (None, None, 0, False, 1)
+    dY2, dcoef, dseg, dS = dpro if dpro is not None else (None, None, 0, 1)
     N = geom[14]
     K = geom[6] * geom[7] * geom[3]
-    key = ("wgrad", tuple(geom), creal, psc is not None)
+    M = geom[0] * geom[4] * geom[5]
+    key = ("wgrad", tuple(geom), creal, psc is not None, dpro is not None)
+
+    def nsplit(v):
+        splits = ops.wgrad_splits(geom, v)
+        if dpro is None:
+            return splits
+        seg_iters = dseg // 64
+        sps = max(1, splits // dS)
+        while seg_iters % sps:
+            sps -= 1
+        return dS * sps
 
     def launch(v, o):
-        splits = ops.wgrad_splits(geom, v)
+        splits = nsplit(v)
         partial = torch.empty((splits * N * K,), device=dY.device, dtype=torch.float32)
-        ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v)
+        ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v,
+                  dY2, dcoef, dseg, dS)
 
     v = tuning.pick(key, range(ops.wgrad_nvariants()), 1 if N <= 64 else 0,
                     lambda vv: launch(vv, torch.empty_like(out)))

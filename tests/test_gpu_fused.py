@@ -68,6 +68,56 @@ def test_dgrad_mode3_epilogue(ops, k, s, p):
     assert _rel(got[1], ref2) < 1e-3
 
 
+@pytest.mark.parametrize("N,H,Ci,Co", [(8, 16, 64, 256), (32, 4, 512, 2048)])
+def test_bn_backward_operand_prologue(ops, N, H, Ci, Co):
+    """conv3's dgrad (PRO=2) and wgrad (DPRO) computing da = A·g + B·a + D in the operand
+    prologue == materialising da with ``bn_bwd_apply`` first (and both vs fp32)."""
+    from simclr_amd.models.fused import FusedStages, _BNState, _ConvSpec
+    torch.manual_seed(4)
+    S = 2
+    conv = torch.nn.Conv2d(Ci, Co, 1, 1, 0, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(_bf(torch.randn_like(conv.weight) / math.sqrt(Ci)).float())
+    g = _bf(torch.randn(N, H, H, Co, device=DEV))
+    a = _bf(torch.randn(N, H, H, Co, device=DEV))
+    xin = _bf(torch.randn(N, H, H, Ci, device=DEV))
+    coef = torch.randn(3 * S * Co, device=DEV) * 0.5
+    a_prev = _bf(torch.randn(N, H, H, Ci, device=DEV))
+    sc = torch.rand(S, Ci, device=DEV) + 0.5
+    sh = torch.randn(S, Ci, device=DEV) * 0.3
+    mi = torch.cat([torch.randn(S, Ci, device=DEV) * 0.2, torch.rand(S, Ci, device=DEV) + 0.5])
+    bs = _BNState(mi.reshape(-1).contiguous(), torch.stack([sc, sh]).reshape(2, S * Ci).contiguous(), 1.0)
+    ex = FusedStages.__new__(FusedStages)
+    ex.bnb_prologue = True
+    cs = _ConvSpec(conv, None, 1, 1, 0)
+    assert ex._bnb_ok(cs, a, S)
+    da = torch.empty_like(a)
+    ops.bn_bwd_apply(g, None, a, coef, S, False, da, None)
+    c = coef.view(3, S, 1, Co)
+    ref_da = (c[0] * g.float().view(S, -1, Co) + c[1] * a.float().view(S, -1, Co) + c[2])
+    assert _rel(da, ref_da.view_as(da)) < 1e-2
+    gm0, p0, nb0 = ex._dgrad(ops, da, cs, a_prev.shape, S, bn_epi=("mask", a_prev, bs))
+    gm1, p1, nb1 = ex._dgrad(ops, g, cs, a_prev.shape, S, bn_epi=("mask", a_prev, bs),
+                             bnb=(a, coef))
+    assert _rel(gm1, gm0) < 1e-2
+    s0 = torch.empty(2 * S * Ci, device=DEV)
+    s1 = torch.empty(2 * S * Ci, device=DEV)
+    ops.bn_reduce(p0, nb0, S, Ci, s0)
+    ops.bn_reduce(p1, nb1, S, Ci, s1)
+    assert _rel(s1, s0) < 2e-2
+    for bnb, dyn in ((None, da), ((a, coef), g)):
+        conv.weight.grad = None
+        ex._wgrad(ops, dyn, xin, cs, bs.ss, S, bnb=bnb)
+        if bnb is None:
+            w0 = conv.weight.grad.clone()
+        else:
+            w1 = conv.weight.grad.clone()
+    xa = torch.relu(xin.float().view(S, -1, Ci) * sc[:, None] + sh[:, None]).reshape(-1, Ci)
+    wref = ref_da.reshape(-1, Co).t() @ _bf(xa).float()
+    assert _rel(w0.view(Co, Ci), wref) < 2e-2
+    assert _rel(w1.view(Co, Ci), w0.view(Co, Ci)) < 1e-2
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_bn_apply_ss_and_finalize_table(ops, mode):
     torch.manual_seed(1)
