@@ -277,10 +277,14 @@ class FusedStages:
 
     def _bnb_ok(self, cs: _ConvSpec, a: torch.Tensor, S: int) -> bool:
         """The BN-backward operand prologue applies to a 1x1 stride-1 conv whose per-segment
-        rows tile evenly (64-row wgrad splits, 64..256-row dgrad tiles)."""
+        rows tile evenly (64-row wgrad splits, 64..256-row dgrad tiles), and pays off only
+        while each dy element is loaded about once: the dgrad re-reads its A operand per
+        output-channel tile and the wgrad its dY operand per input-channel tile, so with
+        ≥ 256 input channels the repeated prologue work outweighs the saved HBM pass
+        (measured on layer3/layer4 of ResNet-50: net loss or break-even)."""
         M = a.numel() // a.shape[-1]
         return (self.bnb_prologue and cs.k == 1 and cs.stride == 1 and M % S == 0
-                and (M // S) % 256 == 0)
+                and (M // S) % 256 == 0 and cs.conv.in_channels <= 128)
 
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
                dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,

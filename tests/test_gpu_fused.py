@@ -90,7 +90,7 @@ def test_bn_backward_operand_prologue(ops, N, H, Ci, Co):
     ex = FusedStages.__new__(FusedStages)
     ex.bnb_prologue = True
     cs = _ConvSpec(conv, None, 1, 1, 0)
-    assert ex._bnb_ok(cs, a, S)
+    assert ex._bnb_ok(cs, a, S) == (Ci <= 128)  # the kernels below run regardless
     da = torch.empty_like(a)
     ops.bn_bwd_apply(g, None, a, coef, S, False, da, None)
     c = coef.view(3, S, 1, Co)
