@@ -274,6 +274,7 @@ void bn_stats(const Tensor& x, int64_t S, const Tensor& partial) {
 void bn_reduce(const Tensor& partial, int64_t nblk, int64_t S, int64_t C, const Tensor& stats) {
   TORCH_CHECK(partial.numel() >= S * nblk * 2 * C && stats.numel() >= 2 * S * C, "bn_reduce sizes");
   const int G = bn_reduce_groups((int)nblk);
+  TORCH_CHECK(G == 1 || C % 4 == 0, "bn_reduce: C must be a multiple of 4 (float4 partial rows)");
   at::Tensor ws;
   float* wsp = nullptr;
   if (G > 1) {
@@ -326,6 +327,8 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
                         const c10::optional<Tensor>& coef) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "bn_reduce_fused: mode");
   TORCH_CHECK(nblk > 0 && partial.numel() >= S * nblk * 2 * C, "bn_reduce_fused: partial size");
+  TORCH_CHECK(C % 4 == 0, "bn_reduce_fused: C must be a multiple of 4 (float4 partial rows)");
+  TORCH_CHECK(S >= 1 && S <= 4, "bn_reduce_fused: at most 4 segments");
   BnReduceFusedParams q;
   q.partial = f32(partial, "partial");
   q.nblk = (int)nblk; q.S = (int)S; q.C = (int)C; q.mode = (int)mode;

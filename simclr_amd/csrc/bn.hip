@@ -6,6 +6,8 @@
 // Layout: x is [R, C] (R = S segments x Rs rows, C % 8 == 0), 16-byte vector accesses,
 // per-thread fixed channel chunk so scale/shift live in registers, fp32 math, deterministic
 // two-level reductions (block partials, then one reduce pass) — no float atomics.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -73,39 +75,53 @@ __global__ __launch_bounds__(256) void k_bn_stats(const uint16_t* __restrict__ x
   }
 }
 
-// Level 1: grid (ceil(C/64), S, G); block = 64 channels x 4 row lanes; each block sums a slice of
-// the nblk partial rows of one segment -> level-2 partials [S][G][2][C].  Enough blocks to spread
-// the (latency-bound) read over the chip; order of summation fixed => deterministic.
+// Level-1 slice of a [S][nblk][2][C] partial array: one block = 64 channels x both halves
+// (Σ, Σ²) = 32 float4 columns x 8 row lanes, summing rows [beg, end) of segment s.  16-byte loads
+// and several rows in flight per thread: a 4 MB partial is read by a few hundred blocks in ~1 µs
+// of DRAM time, so the pass is latency-bound and wants bytes-in-flight (guide §3, R3).
+// Returns (in threads 0..31) the float4 sum of column j = tid: half = j >> 4, c = cg*64 + (j&15)*4.
+__device__ __forceinline__ float4 l1_slice(const float* __restrict__ partial, int nblk, int C,
+                                           int s, int cg, int beg, int end, float4 (*red)[32]) {
+  const int j = threadIdx.x & 31;
+  const int rl = threadIdx.x >> 5;
+  const int c4 = cg * 64 + (j & 15) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 < C) {
+    const float* src = partial + (size_t)s * nblk * 2 * C + (j >> 4) * C + c4;
+#pragma unroll 4
+    for (int i = beg + rl; i < end; i += 8) {
+      const float4 v = *(const float4*)(src + (size_t)i * 2 * C);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[rl][j] = acc;
+  __syncthreads();
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (threadIdx.x < 32) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // fixed order: deterministic
+      const float4 v = red[q][j];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+  }
+  return r;
+}
+
+// Level 1: grid (ceil(C/64), S, G); each block sums a G-th of one segment's partial rows for 64
+// channels -> level-2 partials [S][G][2][C].  Order of summation fixed => deterministic.
 __global__ __launch_bounds__(256) void k_reduce_partials_l1(const float* __restrict__ partial,
                                                             int nblk, int S, int C, int G,
                                                             float* __restrict__ l2) {
-  __shared__ float red[4][64][2];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane = threadIdx.x >> 6;
-  const int s = blockIdx.y, gz = blockIdx.z;
+  __shared__ float4 red[8][32];
+  const int s = blockIdx.y, gz = blockIdx.z, cg = blockIdx.x;
   const int per = (nblk + G - 1) / G;
   const int beg = gz * per;
   const int end = min(nblk, beg + per);
-  float a = 0.f, b = 0.f;
-  if (c < C) {
-    const float* src = partial + (size_t)s * nblk * 2 * C;
-#pragma unroll 4
-    for (int i = beg + lane; i < end; i += 4) {
-      a += src[(size_t)i * 2 * C + c];
-      b += src[(size_t)i * 2 * C + C + c];
-    }
-  }
-  red[lane][threadIdx.x & 63][0] = a;
-  red[lane][threadIdx.x & 63][1] = b;
-  __syncthreads();
-  if (lane == 0 && c < C) {
-    const int t = threadIdx.x & 63;
-    a = red[0][t][0] + red[1][t][0] + red[2][t][0] + red[3][t][0];
-    b = red[0][t][1] + red[1][t][1] + red[2][t][1] + red[3][t][1];
-    float* dst = l2 + (((size_t)s * G + gz) * 2) * C;
-    dst[c] = a;
-    dst[C + c] = b;
-  }
+  const float4 r = l1_slice(partial, nblk, C, s, cg, beg, end, red);
+  const int j = threadIdx.x;
+  const int c4 = cg * 64 + (j & 15) * 4;
+  if (j < 32 && c4 < C)
+    *(float4*)(l2 + (((size_t)s * G + gz) * 2) * C + (j >> 4) * C + c4) = r;
 }
 
 // Level 2: stats[2][S][C] = Σ_g l2[s][g][*][c]
@@ -138,7 +154,7 @@ __global__ void k_reduce_partials(const float* __restrict__ partial, int nblk, i
 // must stay on one stream (it does: the compute stream).
 struct BnReduceArgs {
   const float* partial;
-  int nblk, S, C, G, mode;
+  int nblk, S, C, G, mode, direct;
   float* ws;
   unsigned* tickets;
   float* stats;  // mode 0 out
@@ -157,39 +173,42 @@ struct BnReduceArgs {
   float* coef;
 };
 
+constexpr int kMaxSeg = 4;  // BatchNorm segments (views) per launch handled by the reducer
+
 __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
-  __shared__ float red[4][64][2];
+  __shared__ float4 red4[kMaxSeg * 8][32];
+  __shared__ float fin[kMaxSeg][2][64];
   __shared__ int last;
   const int cl = threadIdx.x & 63;
   const int lane = threadIdx.x >> 6;
   const int cg = blockIdx.x;
   const int c = cg * 64 + cl;
+  const int C = p.C, S = p.S;
+  int G = p.G;
+  const float* src2 = p.ws;  // level-2 rows [S][G][2][C]
+  if (p.direct) {
+    // few partial rows: one block per channel group reads them all, no slices / ticket
+    src2 = p.partial;
+    G = p.nblk;
+  } else {
   const int s = blockIdx.y, gz = blockIdx.z;
-  const int C = p.C, S = p.S, G = p.G;
   const int per = (p.nblk + G - 1) / G;
   const int beg = gz * per;
   const int end = min(p.nblk, beg + per);
-  float a = 0.f, b = 0.f;
-  if (c < C) {
-    const float* src = p.partial + (size_t)s * p.nblk * 2 * C;
-#pragma unroll 4
-    for (int i = beg + lane; i < end; i += 4) {
-      a += src[(size_t)i * 2 * C + c];
-      b += src[(size_t)i * 2 * C + C + c];
-    }
-  }
-  red[lane][cl][0] = a;
-  red[lane][cl][1] = b;
-  __syncthreads();
+  const float4 r = l1_slice(p.partial, p.nblk, C, s, cg, beg, end, red4);
   // ---- publish this slice write-through (sc1: agent-scope relaxed atomic stores), so no
   // release fence is needed — an agent release would write back this XCD's whole dirty L2,
   // which right after a conv epilogue is megabytes (guide §6 Guideline 16, R1)
-  if (lane == 0 && c < C) {
-    a = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
-    b = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
-    float* dst = p.ws + (((size_t)s * G + gz) * 2) * C;
-    __hip_atomic_store(dst + c, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dst + C + c, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  {
+    const int j = threadIdx.x;
+    const int c4 = cg * 64 + (j & 15) * 4;
+    if (j < 32 && c4 < C) {
+      float* dst = p.ws + (((size_t)s * G + gz) * 2) * C + (j >> 4) * C + c4;
+      __hip_atomic_store(dst + 0, r.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + 1, r.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + 2, r.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + 3, r.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains its sc1 stores
   __syncthreads();
@@ -202,39 +221,62 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
   }
   __syncthreads();
   if (!last) return;
-  // consumer: ONE agent acquire (drops this CU's stale L1 lines), then plain, pipelined loads,
-  // the G slices of each segment split over the 4 waves and combined through LDS (fixed order)
+  // consumer: ONE agent acquire (drops this CU's stale L1 lines), then every (segment, slice)
+  // row of the 64-channel group loaded at once by all 256 threads (16-byte loads, all in
+  // flight together: the slices come from other XCDs through memory, so each dependent round
+  // trip costs ~µs) and combined through LDS in a fixed order
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  if (p.mode == 1 && c == 0 && lane == 0 && p.nbt != nullptr) p.nbt[0] += S;  // one per view
-  float rm = 0.f, rv = 0.f, dg = 0.f, db = 0.f, gm = 1.f;
-  if (c < C) {
-    if (p.mode == 1) {
-      rm = p.running_mean ? p.running_mean[c] : 0.f;
-      rv = p.running_var ? p.running_var[c] : 0.f;
-    }
-    if (p.mode == 2) gm = p.gamma ? p.gamma[c] : 1.f;
-  }
-  const float unbias = p.count > 1.f ? p.count / (p.count - 1.f) : 1.f;
-  for (int sg = 0; sg < S; ++sg) {
-    float s1 = 0.f, s2 = 0.f;
-    if (c < C) {
-      for (int g = lane; g < G; g += 4) {
-        const float* src = p.ws + (((size_t)sg * G + g) * 2) * C;
-        s1 += src[c];
-        s2 += src[C + c];
+  }  // !direct
+  {
+    const int j = threadIdx.x & 31, rl = threadIdx.x >> 5;
+    const int c4 = cg * 64 + (j & 15) * 4;
+    float4 acc[kMaxSeg];
+#pragma unroll
+    for (int sg = 0; sg < kMaxSeg; ++sg) acc[sg] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < C) {
+      const float* base = src2 + (j >> 4) * C + c4;
+#pragma unroll 4
+      for (int g = rl; g < G; g += 8) {
+#pragma unroll
+        for (int sg = 0; sg < kMaxSeg; ++sg) {
+          if (sg < S) {
+            const float4 v = *(const float4*)(base + (((size_t)sg * G + g) * 2) * C);
+            acc[sg].x += v.x; acc[sg].y += v.y; acc[sg].z += v.z; acc[sg].w += v.w;
+          }
+        }
       }
     }
-    __syncthreads();
-    red[lane][cl][0] = s1;
-    red[lane][cl][1] = s2;
-    __syncthreads();
-    if (lane != 0 || c >= C) continue;
-    s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
-    s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+#pragma unroll
+    for (int sg = 0; sg < kMaxSeg; ++sg) red4[sg * 8 + rl][j] = acc[sg];  // red4: [kMaxSeg*8][32]
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 * S) {
+    const int j = threadIdx.x & 31, sg = threadIdx.x >> 5;
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 v = red4[sg * 8 + q][j];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    float* f = &fin[sg][j >> 4][(j & 15) * 4];
+    f[0] = r.x; f[1] = r.y; f[2] = r.z; f[3] = r.w;
+  }
+  __syncthreads();
+  if (p.mode == 1 && c == 0 && lane == 0 && p.nbt != nullptr) p.nbt[0] += S;  // one per view
+  if (lane != 0 || c >= C) return;
+  float rm = 0.f, rv = 0.f, dg = 0.f, db = 0.f, gm = 1.f;
+  if (p.mode == 1) {
+    rm = p.running_mean ? p.running_mean[c] : 0.f;
+    rv = p.running_var ? p.running_var[c] : 0.f;
+  }
+  if (p.mode == 2) gm = p.gamma ? p.gamma[c] : 1.f;
+  const float unbias = p.count > 1.f ? p.count / (p.count - 1.f) : 1.f;
+  for (int sg = 0; sg < S; ++sg) {
+    const float s1 = fin[sg][0][cl], s2 = fin[sg][1][cl];
     if (p.mode == 0) {
       p.stats[sg * C + c] = s1;
       p.stats[S * C + sg * C + c] = s2;
@@ -767,10 +809,26 @@ void bn_stats_partial(const uint16_t* x, int R, int C, int S, float* partial, in
   HIP_CHECK_LAUNCH();
 }
 
+int bn_reduce_direct_rows() {
+  static int d = -1;
+  if (d < 0) {
+    const char* e = getenv("SIMCLR_BNRED_DIRECT");
+    d = e ? atoi(e) : 64;  // measured: direct wins only for the smallest partials
+  }
+  return d;
+}
+
 int bn_reduce_groups(int nblk) {
-  if (nblk <= 32) return 1;
-  int g = (nblk + 31) / 32;  // ~32 rows per level-1 block
-  return g > 64 ? 64 : g;
+  static int rows = -1, cap = -1;  // tuning overrides (tools/bench_reduce.py)
+  if (rows < 0) {
+    const char* e = getenv("SIMCLR_BNRED_ROWS");
+    const char* f = getenv("SIMCLR_BNRED_CAP");
+    rows = e ? atoi(e) : 128;  // measured (tools/bench_reduce.py): few slices beat many — the
+    cap = f ? atoi(f) : 16;    // per-group ticket atomics serialise and the consumer reads all
+  }
+  if (nblk <= rows) return 1;
+  int g = (nblk + rows - 1) / rows;  // ~rows partial rows per level-1 block
+  return g > cap ? cap : g;
 }
 
 void bn_reduce_partials(const float* partial, int nblk, int S, int C, float* stats, float* ws,
@@ -802,12 +860,14 @@ void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s) {
   BnReduceArgs a{};
   a.partial = q.partial; a.nblk = q.nblk; a.S = q.S; a.C = q.C; a.mode = q.mode;
   a.G = bn_reduce_groups(q.nblk);
+  a.direct = q.nblk <= bn_reduce_direct_rows();
   a.ws = q.ws; a.tickets = q.tickets; a.stats = q.stats;
   a.count = q.count; a.eps = q.eps; a.momentum = q.momentum;
   a.running_mean = q.running_mean; a.running_var = q.running_var; a.mi = q.mi; a.nbt = q.nbt;
   a.gamma = q.gamma; a.beta = q.beta; a.ss = q.ss;
   a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.coef = q.coef;
-  hipLaunchKernelGGL(k_bn_reduce_fused, dim3((q.C + 63) / 64, q.S, a.G), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_bn_reduce_fused, a.direct ? dim3((q.C + 63) / 64) : dim3((q.C + 63) / 64, q.S, a.G),
+                     dim3(256), 0, s, a);
   HIP_CHECK_LAUNCH();
 }
 

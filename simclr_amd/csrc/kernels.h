@@ -68,6 +68,8 @@ void bn_stats_partial(const uint16_t* x, int R, int C, int S, float* partial, in
                       hipStream_t s);
 int bn_stats_blocks_per_seg(int R, int C, int S);
 int bn_reduce_groups(int nblk);  // level-1 groups; workspace = S*groups*2*C floats
+int bn_reduce_direct_rows();      // bn_reduce_fused: partials with <= this many rows per segment are
+                                  // reduced by one block per channel group (no slices / ticket)
 void bn_reduce_partials(const float* partial, int nblk_per_seg, int S, int C, float* stats,
                         float* ws, hipStream_t s);
 void bn_finalize(const float* stats, int S, int C, float count, float eps, float momentum,
