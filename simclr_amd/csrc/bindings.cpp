@@ -249,6 +249,47 @@ void weight_transform(const Tensor& W, const Tensor& Wt, std::vector<int64_t> p)
                         cur_stream());
 }
 
+// Batched dgrad weight transforms: plan (validate + device descriptor table, eager) and launch.
+// The plan holds raw pointers: the caller keeps every W / Wt tensor alive and unmoved while
+// it is used (FusedStages caches it next to the tensors and rebuilds it when they change).
+Tensor weight_transform_plan(const std::vector<Tensor>& Ws, const std::vector<Tensor>& Wts,
+                             std::vector<int64_t> p) {
+  const size_t n = Ws.size();
+  TORCH_CHECK(n > 0 && Wts.size() == n && p.size() == 10 * n, "weight_transform_plan sizes");
+  Tensor host = at::empty({(int64_t)(n * sizeof(WtDesc) / 8) + 1},
+                          at::TensorOptions().dtype(at::kLong));
+  WtDesc* d = reinterpret_cast<WtDesc*>(host.data_ptr<int64_t>());
+  int blk = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t* q = p.data() + 10 * i;
+    const int Co = q[0], KH = q[1], KW = q[2], Ci = q[3], KHs = q[4], KWs = q[5];
+    TORCH_CHECK(Ws[i].numel() == (int64_t)Co * KH * KW * Ci, "weight_transform_plan: W numel");
+    TORCH_CHECK(Wts[i].numel() == (int64_t)Ci * KHs * KWs * Co, "weight_transform_plan: Wt numel");
+    TORCH_CHECK(Ws[i].device() == Wts[0].device() && Wts[i].device() == Wts[0].device(),
+                "weight_transform_plan: one device");
+    for (int a = 0; a < KHs; ++a)
+      TORCH_CHECK(q[6] + a * q[7] >= 0 && q[6] + a * q[7] < KH, "weight_transform_plan: kh");
+    for (int a = 0; a < KWs; ++a)
+      TORCH_CHECK(q[8] + a * q[9] >= 0 && q[8] + a * q[9] < KW, "weight_transform_plan: kw");
+    const int nb = ((Co + 63) / 64) * ((Ci + 63) / 64) * KHs * KWs;  // 64x64 tiles per tap
+    d[i] = WtDesc{bf(Ws[i], "W"), bfw(Wts[i], "Wt"), Co, KH, KW, Ci, KHs, KWs, (int)q[6],
+                  (int)q[7], (int)q[8], (int)q[9], blk, nb};
+    blk += nb;
+  }
+  // host table [n descriptors | total block count]; the caller moves the descriptors to the
+  // device once and keeps the count on the host (no sync per launch, graph-capturable)
+  host.data_ptr<int64_t>()[n * sizeof(WtDesc) / 8] = blk;
+  return host;
+}
+
+void weight_transform_batch(const Tensor& table, int64_t total_blocks) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.numel() % 8 == 0 &&
+                  table.numel() > 0 && total_blocks > 0,
+              "weight_transform_batch: device descriptors from weight_transform_plan");
+  conv_weight_transform_batch(reinterpret_cast<const WtDesc*>(table.data_ptr<int64_t>()),
+                              (int)(table.numel() / 8), (int)total_blocks, cur_stream());
+}
+
 // ------------------------------------------------------------------------------- batch norm
 void check_rc(const Tensor& x, int64_t S, const char* n) {
   TORCH_CHECK(x.dim() >= 2, n, ": rank");
@@ -607,6 +648,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);
+  m.def("weight_transform_plan(Tensor[] Ws, Tensor[] Wts, int[] p) -> Tensor", &weight_transform_plan);
+  m.def("weight_transform_batch(Tensor table, int total_blocks) -> ()", &weight_transform_batch);
   m.def("bn_blocks(int R, int C, int S) -> int", &bn_blocks);
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);

@@ -738,6 +738,47 @@ __global__ void weight_transform(const uint16_t* __restrict__ W, uint16_t* __res
   }
 }
 
+// All dgrad weight transforms of a step in one launch: a table of WtDesc (built once per weight
+// set, kernels.h), blocks assigned contiguously per descriptor and found by binary search.
+// The weights change only at the optimizer step, so the ~60 per-conv launches collapse into
+// one.  Each block transposes one 64(co) x 64(ci) tile of one (khs, kws) tap through LDS, so
+// both the W reads (along ci) and the Wt writes (along co) are coalesced.
+__global__ __launch_bounds__(256) void weight_transform_batch(const WtDesc* __restrict__ d, int n) {
+  __shared__ uint16_t tile[64][65];
+  int lo = 0, hi = n - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {  // last descriptor with blk0 <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const WtDesc q = d[lo];
+  const int nco = (q.Co + 63) / 64, nci = (q.Ci + 63) / 64;
+  int t = b - q.blk0;
+  const int tco = t % nco;
+  t /= nco;
+  const int tci = t % nci;
+  t /= nci;
+  const int kws = t % q.KWs, khs = t / q.KWs;
+  const int kh = q.kh0 + khs * q.sh, kw = q.kw0 + kws * q.sw;
+  const int co0 = tco * 64, ci0 = tci * 64;
+#pragma unroll 4
+  for (int e = 0; e < 16; ++e) {
+    const int idx = threadIdx.x + 256 * e;
+    const int r = idx >> 6, c = idx & 63;  // r: co, c: ci (consecutive threads along ci)
+    const int co = co0 + r, ci = ci0 + c;
+    if (co < q.Co && ci < q.Ci) tile[r][c] = q.W[(((size_t)co * q.KH + kh) * q.KW + kw) * q.Ci + ci];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int e = 0; e < 16; ++e) {
+    const int idx = threadIdx.x + 256 * e;
+    const int r = idx >> 6, c = idx & 63;  // r: ci, c: co (consecutive threads along co)
+    const int ci = ci0 + r, co = co0 + c;
+    if (co < q.Co && ci < q.Ci)
+      q.Wt[(((size_t)ci * q.KHs + khs) * q.KWs + kws) * q.Co + co] = tile[c][r];
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int PRO, int EPI>
 void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   IgemmArgs a = a0;
@@ -814,6 +855,11 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
 constexpr int WG_VARIANTS[][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {64, 256}, {256, 64}};
 
 }  // namespace
+
+void conv_weight_transform_batch(const WtDesc* d, int n, int total_blocks, hipStream_t s) {
+  hipLaunchKernelGGL(weight_transform_batch, dim3(total_blocks), dim3(256), 0, s, d, n);
+  HIP_CHECK_LAUNCH();
+}
 
 int igemm_num_variants() { return (int)(sizeof(IG_VARIANTS) / sizeof(IG_VARIANTS[0])); }
 int igemm_variant_bm(int v) { return IG_VARIANTS[v][0]; }

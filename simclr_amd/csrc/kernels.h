@@ -60,6 +60,15 @@ int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
                 float* partial, int splits, float* out, int Creal, float beta,
                 const ConvFusion& f, int variant, hipStream_t s);
+// one dgrad weight transform (see weight_transform_batch): Wt[ci][khs][kws][co] =
+// W[co][kh0 + khs*sh][kw0 + kws*sw][ci]; blocks [blk0, blk0 + nblk) of the batch launch
+struct WtDesc {
+  const uint16_t* W;
+  uint16_t* Wt;
+  int Co, KH, KW, Ci, KHs, KWs, kh0, sh, kw0, sw, blk0, nblk;
+};
+static_assert(sizeof(WtDesc) == 64, "WtDesc layout");
+void conv_weight_transform_batch(const WtDesc* d, int n, int total_blocks, hipStream_t s);
 void conv_weight_transform(const uint16_t* W, uint16_t* Wt, int Co, int KH, int KW, int Ci,
                            int KHs, int KWs, int kh0, int sh, int kw0, int sw, hipStream_t s);
 

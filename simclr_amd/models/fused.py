@@ -121,6 +121,11 @@ class FusedStages:
         self.calls = 0
         # BN backward of a bottleneck's conv3 inside conv3's dgrad/wgrad operand prologues
         self.bnb_prologue = os.environ.get("SIMCLR_BNB_PROLOGUE", "1") != "0"
+        # dgrad weight transforms of the whole backbone: one batched launch per backward
+        self._wt_sig = None
+        self._wt_cache = {}
+        self._wt_table = None
+        self._wt_ready = False
         self.blocks: List[_BlockSpec] = []
         for li, layer in enumerate((resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4)):
             for bi, blk in enumerate(layer):
@@ -312,8 +317,8 @@ class FusedStages:
             dx = _empty_nhwc(Nb, H, W, Ci, dev)
         launches = []
         if cs.stride == 1:
-            wt = torch.empty((Ci, KH, KW, Co), device=dev, dtype=torch.bfloat16)
-            ops.weight_transform(w, wt, [Co, KH, KW, Ci, KH, KW, KH - 1, -1, KW - 1, -1])
+            wt = self._dgrad_weight(ops, cs, w, (0, 0),
+                                    [Co, KH, KW, Ci, KH, KW, KH - 1, -1, KW - 1, -1])
             g = [Nb, OH, OW, Co, H, W, KH, KW, 1, 1, 1, 1, -(KH - 1 - cs.pad),
                  -(KW - 1 - cs.pad), Ci, H, W, 1, 1, 0, 0, Ci]
             launches.append((wt, g, Nb * H * W))
@@ -331,8 +336,8 @@ class FusedStages:
                     if nkh == 0 or nkw == 0:
                         zero_needed = True
                         continue
-                    wt = torch.empty((Ci, nkh, nkw, Co), device=dev, dtype=torch.bfloat16)
-                    ops.weight_transform(w, wt, [Co, KH, KW, Ci, nkh, nkw, kh0, 2, kw0, 2])
+                    wt = self._dgrad_weight(ops, cs, w, (r, c),
+                                            [Co, KH, KW, Ci, nkh, nkw, kh0, 2, kw0, 2])
                     ih0 = (r + cs.pad - kh0) // 2
                     iw0 = (c + cs.pad - kw0) // 2
                     g = [Nb, OH, OW, Co, ohc, owc, nkh, nkw, 1, 1, -1, -1, ih0, iw0, Ci,
@@ -383,6 +388,67 @@ class FusedStages:
         if partial2 is not None:
             return dx, (partial, partial2), seg_blocks
         return dx, partial, seg_blocks
+
+    # ------------------------------------------------------------------ dgrad weights
+    @staticmethod
+    def _wt_params(cs: _ConvSpec):
+        """[(parity class, weight_transform params)] of a conv's dgrad: stride 1 → the flipped,
+        transposed kernel; stride 2 → one sub-kernel per (row, col) parity class."""
+        conv = cs.conv
+        Co, Ci, KH, KW = conv.out_channels, conv.in_channels, cs.k, cs.k
+        if cs.stride == 1:
+            return [((0, 0), [Co, KH, KW, Ci, KH, KW, KH - 1, -1, KW - 1, -1])]
+        out = []
+        for r in (0, 1):
+            for c in (0, 1):
+                kh0, kw0 = (r + cs.pad) % 2, (c + cs.pad) % 2
+                nkh = (KH - kh0 + 1) // 2 if kh0 < KH else 0
+                nkw = (KW - kw0 + 1) // 2 if kw0 < KW else 0
+                if nkh and nkw:
+                    out.append(((r, c), [Co, KH, KW, Ci, nkh, nkw, kh0, 2, kw0, 2]))
+        return out
+
+    def prepare_backward(self, ops) -> None:
+        """Transform every conv's dgrad weights in ONE launch (weights change only at the
+        optimizer step).  Needs flat-store-bound bf16 shadows (stable addresses); the plan is
+        built eagerly once and rebuilt if the shadows move — never during graph capture."""
+        convs = [cs for b in self.blocks for cs in (b.convs + ([b.down] if b.down else []))]
+        shadows = []
+        for cs in convs:
+            slot = getattr(cs.conv.weight, "_slot", None)
+            if slot is None or slot.shadow is None:
+                self._wt_ready = False
+                return
+            shadows.append(slot.shadow)
+        sig = tuple(t.data_ptr() for t in shadows)
+        if sig != self._wt_sig:
+            if torch.cuda.is_current_stream_capturing():
+                self._wt_ready = False
+                return
+            Ws, Wts, params, cache = [], [], [], {}
+            for cs, w in zip(convs, shadows):
+                for key, p in self._wt_params(cs):
+                    wt = torch.empty((p[3], p[4], p[5], p[0]), device=w.device,
+                                     dtype=torch.bfloat16)
+                    Ws.append(w)
+                    Wts.append(wt)
+                    params.extend(p)
+                    cache[(id(cs.conv), key)] = wt
+            plan = ops.weight_transform_plan(Ws, Wts, params)
+            self._wt_table = (plan[:-1].to(shadows[0].device), int(plan[-1]), Ws)
+            self._wt_cache = cache
+            self._wt_sig = sig
+        ops.weight_transform_batch(self._wt_table[0], self._wt_table[1])
+        self._wt_ready = True
+
+    def _dgrad_weight(self, ops, cs: _ConvSpec, w, key, p):
+        if getattr(self, "_wt_ready", False):
+            wt = self._wt_cache.get((id(cs.conv), key))
+            if wt is not None and wt.shape[0] == p[3]:
+                return wt
+        wt = torch.empty((p[3], p[4], p[5], p[0]), device=w.device, dtype=torch.bfloat16)
+        ops.weight_transform(w, wt, p)
+        return wt
 
     # ------------------------------------------------------------------ forward / backward
     def forward(self, xn: torch.Tensor) -> Tuple[torch.Tensor, List[_BlockTape]]:
@@ -437,10 +503,12 @@ class FusedStages:
         ops = _ext.ops()
         st = pstate.get()
         S = self.S
+        self.prepare_backward(ops)
         g, pre = gout, None
         for idx in range(len(self.blocks) - 1, -1, -1):
             prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else None
             g, pre = self._block_backward(ops, st, S, self.blocks[idx], tapes[idx], g, pre, prev)
+        self._wt_ready = False  # the optimizer step changes the weights
         return g
 
     def _block_backward(self, ops, st, S, b: _BlockSpec, tp: _BlockTape, g: torch.Tensor,

@@ -271,3 +271,27 @@ def test_bn_reduce_fused_matches_three_launch_path(ops, C, nblk, S):
                             gamma, None, None, dg1, db1, coef1)
         for u, v in ((coef1, coef0), (dg1, dg0), (db1, db0)):
             assert torch.allclose(u, v, rtol=1e-4, atol=1e-3)
+
+
+def test_weight_transform_batch_matches_single(ops):
+    """One batched launch == the per-conv dgrad weight transforms (bitwise), for stride-1 flips
+    and stride-2 parity sub-kernels of 1x1 / 3x3 convs."""
+    from simclr_amd.models.fused import FusedStages, _ConvSpec
+    torch.manual_seed(2)
+    specs = [(64, 64, 3, 1, 1), (256, 64, 1, 1, 0), (128, 256, 3, 2, 1), (512, 256, 1, 2, 0),
+             (2048, 512, 1, 1, 0), (8, 16, 3, 2, 1)]
+    Ws, Wts, params, refs = [], [], [], []
+    for Co, Ci, k, s, p in specs:
+        conv = torch.nn.Conv2d(Ci, Co, k, s, p, bias=False)
+        w = _bf(torch.randn(Co, k, k, Ci, device=DEV))
+        for key, prm in FusedStages._wt_params(_ConvSpec(conv, None, s, k, p)):
+            ref = torch.empty((prm[3], prm[4], prm[5], prm[0]), device=DEV, dtype=torch.bfloat16)
+            ops.weight_transform(w, ref, prm)
+            Ws.append(w)
+            Wts.append(torch.full_like(ref, float("nan")))
+            params.extend(prm)
+            refs.append(ref)
+    plan = ops.weight_transform_plan(Ws, Wts, params)
+    ops.weight_transform_batch(plan[:-1].to(DEV), int(plan[-1]))
+    for got, ref in zip(Wts, refs):
+        assert torch.equal(got, ref)
