@@ -43,7 +43,12 @@ def _init():
         dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("SIMCLR_FORCE_COMM", "0") == "1"
+    if force and world == 1:
+        # 1-rank process group: every collective of the multi-GPU step is still issued
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+    if (world > 1 or force) and not dist.is_initialized():
         # SIMCLR_DIST_BACKEND=gloo rehearses the multi-rank HIP path on one GPU (RCCL refuses
         # two ranks on the same device); the driver's runs use nccl (= RCCL over xGMI).
         be = os.environ.get("SIMCLR_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
@@ -70,8 +75,9 @@ def run_ours(args, rank, world, dev):
     from simclr_amd.utils.misc import seed_everything
 
     st = pstate.set_state(rank=rank, world_size=world, local_rank=int(os.environ.get(
-        "LOCAL_RANK", "0")), group=dist.group.WORLD if world > 1 else None,
-        backend=dist.get_backend() if world > 1 else "none")
+        "LOCAL_RANK", "0")), group=dist.group.WORLD if dist.is_initialized() else None,
+        backend=dist.get_backend() if dist.is_initialized() else "none",
+        force_comm=dist.is_initialized())
     st.device = dev
     pstate.make_stat_group(st)
     ov = [f"experiment.base_cnn={args.model}", f"experiment.batches={args.batch}",
@@ -187,7 +193,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
     rank, world, local, dev = _init()
     if args.graph is None:
-        args.graph = world == 1
+        args.graph = world == 1 and not dist.is_initialized()
     if args.impl == "ours":
         dt, loss = run_ours(args, rank, world, dev)
     else:
@@ -244,7 +250,7 @@ def main(argv=None):
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -64,7 +64,7 @@ class _NTXentHipFn(torch.autograd.Function):
         zn = torch.empty((R, D), device=dev, dtype=torch.float32)
         inv = torch.empty((R,), device=dev, dtype=torch.float32)
         ops.nt_normalize(zb, zn, inv)
-        if gather and st.world_size > 1:
+        if gather and st.comm:
             zall = torch.empty((st.world_size * R, D), device=dev, dtype=torch.float32)
             dist.all_gather_into_tensor(zall, zn, group=st.group)
             col_offset = st.rank * R
@@ -107,7 +107,7 @@ class _NTXentHipFn(torch.autograd.Function):
         d_cols = torch.empty((Ccols, D), device=dev, dtype=torch.float32)
         ops.nt_backward_part(False, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part2,
                              s_col, d_cols)
-        if gather and st.world_size > 1:
+        if gather and st.comm:
             # only this rank's slice of the column gradient is needed: reduce-scatter moves
             # 1/W of an all-reduce's bytes over the xGMI links
             mine = torch.empty((R, D), device=dev, dtype=torch.float32)

@@ -51,7 +51,7 @@ def _empty_nhwc(n, h, w, c, dev, dtype=torch.bfloat16):
 
 
 def _allreduce(t: torch.Tensor, st) -> None:
-    if st.world_size > 1:
+    if st.comm:
         dist.all_reduce(t, group=st.stats_group)
 
 
@@ -192,7 +192,7 @@ class FusedStages:
         count = float(rows_seg * st.world_size)
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ss = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        if st.world_size == 1:  # one launch: reduce + finalize (last-arriver)
+        if not st.comm:  # one launch: reduce + finalize (last-arriver)
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
                                 bn.weight.detach(), bn.bias.detach(), ss)
@@ -231,7 +231,7 @@ class FusedStages:
         independent work (a weight gradient) before ``_bn_bwd_finish``.  Single GPU: nothing
         to wait for (one fused launch in the finish)."""
         C = bn.num_features
-        if st.world_size == 1:
+        if not st.comm:
             return ("local", bn, partial, nblk_seg, bs)
         dev = partial.device
         sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)

@@ -33,7 +33,7 @@ def _empty_like_cl(x: torch.Tensor) -> torch.Tensor:
 
 
 def _allreduce(t: torch.Tensor, st) -> None:
-    if st.world_size > 1:
+    if st.comm:
         dist.all_reduce(t, group=st.stats_group)
 
 
@@ -63,7 +63,7 @@ class BatchNormHipFn(torch.autograd.Function):
             ops.bn_stats(xr, S, partial)
         count = float((R // S) * st.world_size)
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        if st.world_size == 1:
+        if not st.comm:
             ops.bn_reduce_fused(partial, nblk, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked)
         else:
@@ -99,7 +99,7 @@ class BatchNormHipFn(torch.autograd.Function):
         dgamma, gslot = _grad_out(weight)
         dbeta, bslot = _grad_out(ctx.bias)
         coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
-        if st.world_size == 1:
+        if not st.comm:
             ops.bn_reduce_fused(partial, nblk, S, C, 2, None, count, 0.0, 0.0, None, None, mi,
                                 None, weight.detach(), None, None, dgamma, dbeta, coef)
         else:

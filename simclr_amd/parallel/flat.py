@@ -88,6 +88,7 @@ class FlatParamStore:
         st = pstate.get()
         self.group = group if group is not None else st.group
         self.world_size = world_size if world_size is not None else st.world_size
+        self.comm = self.world_size > 1 or (world_size is None and group is None and st.comm)
         self._build_buckets(bucket_mb, first_bucket_mb)
         self._comm_stream = None
         self._works: List = []
@@ -138,7 +139,7 @@ class FlatParamStore:
         self._works = []
 
     def mark_ready(self, index: int) -> None:
-        if self.world_size <= 1 or self._seen[index]:
+        if not self.comm or self._seen[index]:
             return
         self._seen[index] = True
         b = self.bucket_of[index]
@@ -164,7 +165,7 @@ class FlatParamStore:
 
     def finish(self) -> None:
         """Flush unlaunched buckets (unused params), then make the compute stream wait."""
-        if self.world_size <= 1:
+        if not self.comm:
             return
         while self._next_launch < len(self.buckets):
             self._launch(self._next_launch)
@@ -177,7 +178,7 @@ class FlatParamStore:
 
     def broadcast_from(self, src: int = 0) -> None:
         """Make all ranks start from rank ``src``'s parameters and buffers (DDP ctor semantics)."""
-        if self.world_size <= 1:
+        if not self.comm:
             return
         dist.broadcast(self.master, src=src, group=self.group)
         for b in self.model.buffers():

@@ -23,6 +23,9 @@ class ParallelState:
     # second communicator for the latency-critical BatchNorm statistics all-reduces, so they
     # never queue behind a multi-MiB gradient-bucket all-reduce on the same RCCL stream
     stat_group: Optional[object] = None
+    # run every collective even at world_size 1 (a 1-rank RCCL group): exercises the
+    # multi-GPU code path (comm streams, async handles, the stats communicator) on one GPU
+    force_comm: bool = False
 
     @property
     def stats_group(self):
@@ -31,6 +34,11 @@ class ParallelState:
     @property
     def distributed(self) -> bool:
         return self.world_size > 1
+
+    @property
+    def comm(self) -> bool:
+        """True when the step issues collectives (multi-rank, or ``force_comm``)."""
+        return self.world_size > 1 or (self.force_comm and self.group is not None)
 
 
 _STATE = ParallelState()
@@ -48,7 +56,7 @@ def set_state(**kw) -> ParallelState:
 
 def make_stat_group(st: "ParallelState") -> None:
     """Create the BN-statistics communicator (collective call: every rank, same order)."""
-    if st.world_size > 1 and st.stat_group is None and dist.is_initialized():
+    if st.comm and st.stat_group is None and dist.is_initialized():
         st.stat_group = dist.new_group(list(range(st.world_size)))
 
 

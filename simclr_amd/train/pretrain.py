@@ -124,7 +124,10 @@ class Trainer:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._static_x = x.clone()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # with collectives in the step, the RCCL watchdog thread polls work events while the
+        # capture is open: thread-local capture mode keeps those queries legal
+        mode = "thread_local" if self.st.comm else "global"
+        with torch.cuda.graph(g, capture_error_mode=mode):
             self._static_loss = self._step_body(self._static_x)
         self.opt.host_step -= 1  # the captured body incremented it once; replays add per step
         self.graph = g
