@@ -117,6 +117,9 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int bm = igemm_variant_bm((int)variant);
+  if (igemm_variant_glds((int)variant))
+    TORCH_CHECK(g.C % 64 == 0 && !(pro_sc.has_value() && pro_sc->defined()),
+                "igemm: LDS-DMA variant needs C % 64 == 0 and no operand prologue");
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
   const bool has_stats = stats.has_value() && stats->defined();
   if (has_stats && stats_seg_blocks == 0)
@@ -188,6 +191,7 @@ int64_t igemm_bm(int64_t N) { return igemm_block_m((int)N); }
 int64_t igemm_nvariants() { return igemm_num_variants(); }
 int64_t igemm_vbm(int64_t v) { return igemm_variant_bm((int)v); }
 int64_t igemm_vbn(int64_t v) { return igemm_variant_bn((int)v); }
+bool igemm_vglds(int64_t v) { return igemm_variant_glds((int)v); }
 int64_t wgrad_nvariants() { return wgrad_num_variants(); }
 
 int64_t wgrad_nsplit(std::vector<int64_t> gv, int64_t variant) {
@@ -644,6 +648,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
   m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);
   m.def("igemm_variant_bn(int v) -> int", &igemm_vbn);
+  m.def("igemm_variant_glds(int v) -> bool", &igemm_vglds);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);

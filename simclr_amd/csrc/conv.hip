@@ -102,6 +102,183 @@ __device__ __forceinline__ u32x4 bnbwd8(u32x4 g, u32x4 x, const float* A, const 
   return w;
 }
 
+// Epilogue shared by the igemm kernels: bias, bf16 round, LDS-staged 16-B row stores, fused
+// elementwise modes 1-5 and the per-block BatchNorm partial statistics (see IgemmArgs).
+template <int BM, int BN, int WM, int WN, int NT, int EPI>
+__device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
+                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                               char* smem, int m0, int n0, int mb) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  static_assert(BN / 8 <= NT && NT % (BN / 8) == 0 && BN <= NT, "epilogue thread mapping");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int OHW = p.OH * p.OW;
+  constexpr int CST = BN + 8;  // padded row stride (elements)
+  uint16_t* Cs = (uint16_t*)smem;
+  // the MFMAs compute C^T fragments (B operand first), so each lane holds 4 consecutive
+  // channels of one output row: one 8-byte LDS store per fragment instead of four 2-byte ones
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int col = wn * TN + fn * 16 + (lane >> 4) * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias != nullptr && n0 + col < p.N) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[i] = p.bias[n0 + col + i];
+    }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int row = wm * TM + fm * 16 + (lane & 15);
+      const u32x2 w = {pack2bf(acc[fm][fn][0] + bv[0], acc[fm][fn][1] + bv[1]),
+                       pack2bf(acc[fm][fn][2] + bv[2], acc[fm][fn][3] + bv[3])};
+      *(u32x2*)(Cs + row * CST + col) = w;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;            // 16-B chunks per row
+  constexpr int RSTEP = NT / CPR;        // rows per pass
+  const int ch = tid % CPR;
+  const int r0 = tid / CPR;
+  float s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+  constexpr bool two = EPI == 5;  // mode 4 + the producer's downsample-BN stream
+  const int n = n0 + ch * 8;
+  const int seg = p.seg_rows > 0 ? m0 / p.seg_rows : 0;  // block-uniform (host guarantees)
+  float esc[8], esh[8], emu[8], einv[8], emu2[8], einv2[8];
+  if (EPI == 3 || EPI == 4 || EPI == 5) {
+    const int S = p.epi_S;
+    const int cb = n < p.N ? n : 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (EPI == 3) {
+        esc[e] = p.epi_ss[seg * p.N + cb + e];
+        esh[e] = p.epi_ss[(S + seg) * p.N + cb + e];
+      }
+      emu[e] = p.epi_mi[seg * p.N + cb + e];
+      einv[e] = p.epi_mi[(S + seg) * p.N + cb + e];
+      if (two) {
+        emu2[e] = p.epi_mi2[seg * p.N + cb + e];
+        einv2[e] = p.epi_mi2[(S + seg) * p.N + cb + e];
+      }
+    }
+  }
+  for (int row = r0; row < BM; row += RSTEP) {
+    const int m = m0 + row;
+    if (m >= p.M || n >= p.N) continue;
+    u32x4 v = *(const u32x4*)(Cs + row * CST + ch * 8);
+    size_t o;
+    if (p.direct_out) {
+      o = (size_t)m * p.ldo + n;
+    } else {
+      const int img = m / OHW;
+      const int rem = m - img * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      o = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
+    }
+    if (EPI == 1) {
+      const u32x4 r = *(const u32x4*)(p.epi_a + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
+    } else if (EPI == 2) {
+      const u32x4 d = *(const u32x4*)(p.epi_a + o);
+      const u32x4 y = *(const u32x4*)(p.epi_b + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = lo_bf(y[e]) > 0.f ? lo_bf(d[e]) : 0.f;
+        const float b = hi_bf(y[e]) > 0.f ? hi_bf(d[e]) : 0.f;
+        v[e] = pack2bf(lo_bf(v[e]) + a, hi_bf(v[e]) + b);
+      }
+    } else if (EPI == 3) {
+      const u32x4 y = *(const u32x4*)(p.epi_b + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y0 = lo_bf(y[e]), y1 = hi_bf(y[e]);
+        const float g0 = y0 * esc[2 * e] + esh[2 * e] > 0.f ? lo_bf(v[e]) : 0.f;
+        const float g1 = y1 * esc[2 * e + 1] + esh[2 * e + 1] > 0.f ? hi_bf(v[e]) : 0.f;
+        v[e] = pack2bf(g0, g1);  // exact: g is 0 or an already-rounded bf16 value
+        if (p.stats != nullptr) {
+          s1[2 * e] += g0; s2[2 * e] += g0 * ((y0 - emu[2 * e]) * einv[2 * e]);
+          s1[2 * e + 1] += g1; s2[2 * e + 1] += g1 * ((y1 - emu[2 * e + 1]) * einv[2 * e + 1]);
+        }
+      }
+    } else if (EPI == 4 || EPI == 5) {
+      const u32x4 r = *(const u32x4*)(p.epi_a + o);
+      const u32x4 xa = *(const u32x4*)(p.epi_c + o);
+      unsigned bits = 0;
+      if (p.epi_mask != nullptr) {
+        bits = p.epi_mask[o >> 3];
+      } else {
+        const u32x4 y = *(const u32x4*)(p.epi_b + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bits |= (lo_bf(y[e]) > 0.f ? 1u : 0u) << (2 * e) | (hi_bf(y[e]) > 0.f ? 2u : 0u) << (2 * e);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t sum = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
+        const float g0 = (bits >> (2 * e)) & 1u ? lo_bf(sum) : 0.f;
+        const float g1 = (bits >> (2 * e + 1)) & 1u ? hi_bf(sum) : 0.f;
+        v[e] = pack2bf(g0, g1);
+        if (p.stats != nullptr) {
+          s1[2 * e] += g0; s2[2 * e] += g0 * ((lo_bf(xa[e]) - emu[2 * e]) * einv[2 * e]);
+          s1[2 * e + 1] += g1;
+          s2[2 * e + 1] += g1 * ((hi_bf(xa[e]) - emu[2 * e + 1]) * einv[2 * e + 1]);
+        }
+      }
+      if (two) {
+        const u32x4 xd = *(const u32x4*)(p.epi_c2 + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g0 = lo_bf(v[e]), g1 = hi_bf(v[e]);
+          s3[2 * e] += g0 * ((lo_bf(xd[e]) - emu2[2 * e]) * einv2[2 * e]);
+          s3[2 * e + 1] += g1 * ((hi_bf(xd[e]) - emu2[2 * e + 1]) * einv2[2 * e + 1]);
+        }
+      }
+    }
+    *(u32x4*)(p.out + o) = v;
+    if (EPI < 3 && p.stats != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = lo_bf(v[e]), b = hi_bf(v[e]);
+        s1[2 * e] += a; s2[2 * e] += a * a;
+        s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
+      }
+    }
+  }
+  if (p.stats != nullptr) {
+    __syncthreads();
+    constexpr int NS = two ? 3 : 2;
+    float* red = (float*)smem;  // [RSTEP][BN][NS]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(r0 * BN + ch * 8 + e) * NS + 0] = s1[e];
+      red[(r0 * BN + ch * 8 + e) * NS + 1] = s2[e];
+      if (two) red[(r0 * BN + ch * 8 + e) * NS + 2] = s3[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < p.N) {
+      float a = 0.f, b = 0.f, d = 0.f;
+      for (int r = 0; r < RSTEP; ++r) {
+        a += red[(r * BN + tid) * NS + 0];
+        b += red[(r * BN + tid) * NS + 1];
+        if (two) d += red[(r * BN + tid) * NS + 2];
+      }
+      const int blk = p.stats_seg_blocks > 0
+                          ? seg * p.stats_seg_blocks + p.stats_base + (m0 - seg * p.seg_rows) / BM
+                          : mb;
+      p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
+      p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
+      if (two) {
+        p.stats2[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
+        p.stats2[((size_t)blk * 2 + 1) * p.N + n0 + tid] = d;
+      }
+    }
+  }
+}
+
 // PRO: 0 none, 1 BN-apply + ReLU prologue, 2 BN-backward prologue (two operands)
 template <int BM, int BN, int WM, int WN, int PRO, int EPI>
 __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(IgemmArgs p) {
@@ -252,171 +429,144 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
     }
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
 
-  // ---------------- epilogue: bias, bf16 round, LDS-staged row stores, BN partial stats
-  constexpr int CST = BN + 8;  // padded row stride (elements)
-  uint16_t* Cs = (uint16_t*)smem;
+  igemm_epilogue<BM, BN, WM, WN, 256, EPI>(p, acc, smem, m0, n0, mb);
+}
+
+// 16-byte buffer load straight into LDS (buffer_load_dwordx4 ... lds): lane l's bytes land at
+// lds + 16*l (wave-uniform base); an out-of-range offset writes zeros.  The builtin exists only
+// in the device pass (the host pass of a kernel that names it would drop the kernel's stub).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LDS_PTR(void, lds), 16, off, 0, 0, 0);
+#endif
+}
+
+// ---------------------------------------------------------------------- igemm, LDS-DMA staged
+// Large-tile implicit GEMM for the compute-bound convolutions (no operand prologue): both
+// operands go HBM/L2 → LDS with buffer_load_dwordx4 … lds (no VGPR round trip, no ds_write
+// pass; the LDS-write pass was the register-staged kernel's co-bottleneck with the ds_reads).
+// One wave-instruction fills 8 rows x 128 B of the [rows][64] tile image; the XOR chunk swizzle
+// of the image is produced by permuting each lane's SOURCE chunk (the LDS side of a DMA is
+// lane-linear), so fragment reads are the same conflict-free ds_read_b128 as igemm_nt.
+// Out-of-range rows / padding taps use an out-of-range buffer offset: the DMA writes zeros.
+// Pipeline: 2 LDS stages, BK = 64; the DMA of tile k+1 is issued right after the barrier that
+// publishes tile k and runs under tile k's MFMAs; one vmcnt(0) + barrier per k-tile.
+// Host guarantees: C % 64 == 0 (a 64-wide K slice is one tap), no prologue.
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // DMA instructions per wave per tile
+  static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "glds tiling");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* As = (uint16_t*)smem;   // [2][BM][64]
+  uint16_t* Bs = As + 2 * BM * 64;  // [2][BN][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mb = lbid / p.nNb, nb = lbid % p.nNb;
+  const int m0 = mb * BM, n0 = nb * BN;
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+
+  // lane → (row within its 8-row piece, physical chunk); the logical chunk it fetches is
+  // pch ^ (row & 7) = pch ^ lrow (every piece starts at a multiple of 8 rows)
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int lch = pch ^ lrow;
+  const int OHW = p.OH * p.OW;
+  int a_pix[AI], a_ih[AI], a_iw[AI];
 #pragma unroll
-  for (int fn = 0; fn < FN; ++fn) {
-    const int col = wn * TN + fn * 16 + (lane & 15);
-    const float bv = (p.bias != nullptr && n0 + col < p.N) ? p.bias[n0 + col] : 0.f;
+  for (int j = 0; j < AI; ++j) {
+    const int m = m0 + (j * NW + wid) * 8 + lrow;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
+    const int n = mm / OHW;
+    const int rem = mm - n * OHW;
+    const int oh = rem / p.OW;
+    const int ow = rem - oh * p.OW;
+    a_pix[j] = n * p.IH * p.IW;
+    a_ih[j] = ok ? oh * p.ish + p.ih0 : -(1 << 28);  // invalid rows fail the bounds test
+    a_iw[j] = ow * p.isw + p.iw0;
+  }
+  uint32_t b_off[BI];
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
+  for (int j = 0; j < BI; ++j) {
+    const int nrow = n0 + (j * NW + wid) * 8 + lrow;
+    b_off[j] = nrow < p.N ? (uint32_t)(nrow * p.K + lch * 8) * 2u : p.b_bytes;
+  }
+  const uint32_t OOB_A = p.a_bytes;
+
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * 64;
+    const int tap = k0 / p.C;  // wave-uniform
+    const int ci = k0 - tap * p.C + lch * 8;
+    const int kh = tap / p.KW;
+    const int kw = tap - kh * p.KW;
+    const int dih = kh * p.dh, diw = kw * p.dw;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * TM + fm * 16 + (lane >> 4) * 4 + i;
-        Cs[row * CST + col] = f2bf(acc[fm][fn][i] + bv);
+    for (int j = 0; j < AI; ++j) {
+      const int ih = a_ih[j] + dih;
+      const int iw = a_iw[j] + diw;
+      const bool ok = (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      const uint32_t off =
+          ok ? (uint32_t)(((a_pix[j] + ih * p.IW + iw) * p.C + ci) * 2) : OOB_A;
+      dma16(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      dma16(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)k0 * 2u);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / 64;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile kt visible to every wave; every wave is done reading buffer cur^1
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const uint16_t* Ab = As + cur * BM * 64;
+    const uint16_t* Bb = Bs + cur * BN * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int row = wm * TM + fm * 16 + (lane & 15);
+        const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
+        af[fm] = *(const bf16x8*)(Ab + row * 64 + ch * 8);
       }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int row = wn * TN + fn * 16 + (lane & 15);
+        const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
+        bfr[fn] = *(const bf16x8*)(Bb + row * 64 + ch * 8);
+      }
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
     }
   }
-  __syncthreads();
-  constexpr int CPR = BN / 8;            // 16-B chunks per row
-  constexpr int RSTEP = 256 / CPR;       // rows per pass
-  const int ch = tid % CPR;
-  const int r0 = tid / CPR;
-  float s1[8], s2[8], s3[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
-  constexpr bool two = EPI == 5;  // mode 4 + the producer's downsample-BN stream
-  const int n = n0 + ch * 8;
-  const int seg = p.seg_rows > 0 ? m0 / p.seg_rows : 0;  // block-uniform (host guarantees)
-  float esc[8], esh[8], emu[8], einv[8], emu2[8], einv2[8];
-  if (EPI == 3 || EPI == 4 || EPI == 5) {
-    const int S = p.epi_S;
-    const int cb = n < p.N ? n : 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (EPI == 3) {
-        esc[e] = p.epi_ss[seg * p.N + cb + e];
-        esh[e] = p.epi_ss[(S + seg) * p.N + cb + e];
-      }
-      emu[e] = p.epi_mi[seg * p.N + cb + e];
-      einv[e] = p.epi_mi[(S + seg) * p.N + cb + e];
-      if (two) {
-        emu2[e] = p.epi_mi2[seg * p.N + cb + e];
-        einv2[e] = p.epi_mi2[(S + seg) * p.N + cb + e];
-      }
-    }
-  }
-  for (int row = r0; row < BM; row += RSTEP) {
-    const int m = m0 + row;
-    if (m >= p.M || n >= p.N) continue;
-    u32x4 v = *(const u32x4*)(Cs + row * CST + ch * 8);
-    size_t o;
-    if (p.direct_out) {
-      o = (size_t)m * p.ldo + n;
-    } else {
-      const int img = m / OHW;
-      const int rem = m - img * OHW;
-      const int oh = rem / p.OW;
-      const int ow = rem - oh * p.OW;
-      o = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
-    }
-    if (EPI == 1) {
-      const u32x4 r = *(const u32x4*)(p.epi_a + o);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        v[e] = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
-    } else if (EPI == 2) {
-      const u32x4 d = *(const u32x4*)(p.epi_a + o);
-      const u32x4 y = *(const u32x4*)(p.epi_b + o);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = lo_bf(y[e]) > 0.f ? lo_bf(d[e]) : 0.f;
-        const float b = hi_bf(y[e]) > 0.f ? hi_bf(d[e]) : 0.f;
-        v[e] = pack2bf(lo_bf(v[e]) + a, hi_bf(v[e]) + b);
-      }
-    } else if (EPI == 3) {
-      const u32x4 y = *(const u32x4*)(p.epi_b + o);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float y0 = lo_bf(y[e]), y1 = hi_bf(y[e]);
-        const float g0 = y0 * esc[2 * e] + esh[2 * e] > 0.f ? lo_bf(v[e]) : 0.f;
-        const float g1 = y1 * esc[2 * e + 1] + esh[2 * e + 1] > 0.f ? hi_bf(v[e]) : 0.f;
-        v[e] = pack2bf(g0, g1);  // exact: g is 0 or an already-rounded bf16 value
-        if (p.stats != nullptr) {
-          s1[2 * e] += g0; s2[2 * e] += g0 * ((y0 - emu[2 * e]) * einv[2 * e]);
-          s1[2 * e + 1] += g1; s2[2 * e + 1] += g1 * ((y1 - emu[2 * e + 1]) * einv[2 * e + 1]);
-        }
-      }
-    } else if (EPI == 4 || EPI == 5) {
-      const u32x4 r = *(const u32x4*)(p.epi_a + o);
-      const u32x4 xa = *(const u32x4*)(p.epi_c + o);
-      unsigned bits = 0;
-      if (p.epi_mask != nullptr) {
-        bits = p.epi_mask[o >> 3];
-      } else {
-        const u32x4 y = *(const u32x4*)(p.epi_b + o);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          bits |= (lo_bf(y[e]) > 0.f ? 1u : 0u) << (2 * e) | (hi_bf(y[e]) > 0.f ? 2u : 0u) << (2 * e);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t sum = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
-        const float g0 = (bits >> (2 * e)) & 1u ? lo_bf(sum) : 0.f;
-        const float g1 = (bits >> (2 * e + 1)) & 1u ? hi_bf(sum) : 0.f;
-        v[e] = pack2bf(g0, g1);
-        if (p.stats != nullptr) {
-          s1[2 * e] += g0; s2[2 * e] += g0 * ((lo_bf(xa[e]) - emu[2 * e]) * einv[2 * e]);
-          s1[2 * e + 1] += g1;
-          s2[2 * e + 1] += g1 * ((hi_bf(xa[e]) - emu[2 * e + 1]) * einv[2 * e + 1]);
-        }
-      }
-      if (two) {
-        const u32x4 xd = *(const u32x4*)(p.epi_c2 + o);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float g0 = lo_bf(v[e]), g1 = hi_bf(v[e]);
-          s3[2 * e] += g0 * ((lo_bf(xd[e]) - emu2[2 * e]) * einv2[2 * e]);
-          s3[2 * e + 1] += g1 * ((hi_bf(xd[e]) - emu2[2 * e + 1]) * einv2[2 * e + 1]);
-        }
-      }
-    }
-    *(u32x4*)(p.out + o) = v;
-    if (EPI < 3 && p.stats != nullptr) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = lo_bf(v[e]), b = hi_bf(v[e]);
-        s1[2 * e] += a; s2[2 * e] += a * a;
-        s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
-      }
-    }
-  }
-  if (p.stats != nullptr) {
-    __syncthreads();
-    constexpr int NS = two ? 3 : 2;
-    float* red = (float*)smem;  // [RSTEP][BN][NS]
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(r0 * BN + ch * 8 + e) * NS + 0] = s1[e];
-      red[(r0 * BN + ch * 8 + e) * NS + 1] = s2[e];
-      if (two) red[(r0 * BN + ch * 8 + e) * NS + 2] = s3[e];
-    }
-    __syncthreads();
-    if (tid < BN && n0 + tid < p.N) {
-      float a = 0.f, b = 0.f, d = 0.f;
-      for (int r = 0; r < RSTEP; ++r) {
-        a += red[(r * BN + tid) * NS + 0];
-        b += red[(r * BN + tid) * NS + 1];
-        if (two) d += red[(r * BN + tid) * NS + 2];
-      }
-      const int blk = p.stats_seg_blocks > 0
-                          ? seg * p.stats_seg_blocks + p.stats_base + (m0 - seg * p.seg_rows) / BM
-                          : mb;
-      p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
-      p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
-      if (two) {
-        p.stats2[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
-        p.stats2[((size_t)blk * 2 + 1) * p.N + n0 + tid] = d;
-      }
-    }
-  }
+  __syncthreads();  // the epilogue reuses the staging LDS
+  igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb);
 }
 
 // ------------------------------------------------------------------------------------ wgrad
@@ -794,6 +944,37 @@ void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+template <int BM, int BN, int WM, int WN, int EPI>
+void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
+  IgemmArgs a = a0;
+  a.nMb = (a.M + BM - 1) / BM;
+  a.nNb = (a.N + BN - 1) / BN;
+  constexpr int NT = 64 * WM * WN;
+  size_t lds = (size_t)2 * (BM + BN) * 64 * 2;
+  const size_t cst = (size_t)BM * (BN + 8) * 2;
+  const size_t red = (size_t)(NT / (BN / 8)) * BN * 3 * 4;
+  if (cst > lds) lds = cst;
+  if (red > lds) lds = red;
+  hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, EPI>), dim3(a.nMb * a.nNb), dim3(NT), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_glds(const IgemmArgs& a, hipStream_t s) {
+  switch (a.epi_mode) {
+    case 1: launch_glds_t<BM, BN, WM, WN, 1>(a, s); break;
+    case 2: launch_glds_t<BM, BN, WM, WN, 2>(a, s); break;
+    case 3: launch_glds_t<BM, BN, WM, WN, 3>(a, s); break;
+    case 4:
+      if (a.stats2 != nullptr)
+        launch_glds_t<BM, BN, WM, WN, 5>(a, s);
+      else
+        launch_glds_t<BM, BN, WM, WN, 4>(a, s);
+      break;
+    default: launch_glds_t<BM, BN, WM, WN, 0>(a, s); break;
+  }
+}
+
 // compile-time fusion modes (prologue x epilogue), so each launch carries only its own work
 template <int BM, int BN, int WM, int WN>
 void launch_igemm(const IgemmArgs& a, hipStream_t s) {
@@ -850,8 +1031,11 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
 // tile variants: {BM, BN}
 // wide-N / wide-K tiles (5, 6 and wgrad 4, 5) cover a whole small output dimension in one tile,
 // so the other operand is streamed from HBM once instead of N/BN (K/BKK) times
+// variants >= IG_GLDS0 are the LDS-DMA kernel (igemm_glds): no prologue, C % 64 == 0
 constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {64, 64},
-                                  {128, 256}, {64, 256}};
+                                  {128, 256}, {64, 256},
+                                  {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256}};
+constexpr int IG_GLDS0 = 7;
 constexpr int WG_VARIANTS[][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {64, 256}, {256, 64}};
 
 }  // namespace
@@ -865,6 +1049,7 @@ int igemm_num_variants() { return (int)(sizeof(IG_VARIANTS) / sizeof(IG_VARIANTS
 int igemm_variant_bm(int v) { return IG_VARIANTS[v][0]; }
 int igemm_variant_bn(int v) { return IG_VARIANTS[v][1]; }
 int igemm_default_variant(int N) { return N <= 64 ? 1 : 0; }
+bool igemm_variant_glds(int v) { return v >= IG_GLDS0 && v < igemm_num_variants(); }
 int igemm_block_m(int N) { return igemm_variant_bm(igemm_default_variant(N)); }
 
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
@@ -891,7 +1076,16 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
+  if (igemm_variant_glds(variant) && (a.pro_sc != nullptr || g.C % 64 != 0)) {
+    fprintf(stderr, "igemm: LDS-DMA variant %d needs C %% 64 == 0 and no prologue\n", variant);
+    abort();  // the bindings reject this; never silently change BM (stats layout)
+  }
   switch (variant) {
+    case 7: launch_glds<256, 256, 2, 4>(a, s); break;
+    case 8: launch_glds<256, 128, 4, 2>(a, s); break;
+    case 9: launch_glds<256, 64, 4, 1>(a, s); break;
+    case 10: launch_glds<128, 128, 2, 2>(a, s); break;
+    case 11: launch_glds<128, 256, 2, 4>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;

@@ -50,6 +50,7 @@ int igemm_num_variants();
 int igemm_variant_bm(int v);
 int igemm_variant_bn(int v);
 int igemm_default_variant(int N);
+bool igemm_variant_glds(int v);  // LDS-DMA variant: no prologue, needs C % 64 == 0
 int igemm_block_m(int N);
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
                    uint16_t* out, const float* bias, float* stats, const ConvFusion& f,

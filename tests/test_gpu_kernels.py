@@ -268,7 +268,7 @@ def test_igemm_variants_prologue_epilogue(ops, k, s, p):
     refn = ref.permute(0, 2, 3, 1)
     for v in range(ops.igemm_nvariants()):
         bm = ops.igemm_variant_bm(v)
-        if (M // S) % bm:
+        if (M // S) % bm or ops.igemm_variant_glds(v):
             continue
         out = torch.empty(N, OH, OW, Co, device=DEV, dtype=torch.bfloat16)
         ops.igemm(xn, wo, out, None, None, g, sc, sh, M // S, True, 0, None, None, v)
@@ -290,3 +290,92 @@ def test_igemm_variants_prologue_epilogue(ops, k, s, p):
         out = torch.empty(Co, k, k, C, device=DEV)
         ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, sc, sh, M // S, True, S, v)
         assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, v
+
+
+def _glds_variants(ops):
+    return [v for v in range(ops.igemm_nvariants()) if ops.igemm_variant_glds(v)]
+
+
+@pytest.mark.parametrize("k,s,p,C,Co", [(1, 1, 0, 64, 256), (3, 1, 1, 64, 64), (3, 2, 1, 128, 192),
+                                         (1, 2, 0, 128, 128), (3, 1, 1, 128, 512)])
+def test_igemm_glds_variants(ops, k, s, p, C, Co):
+    """The LDS-DMA kernel (igemm_glds): every tile variant against an fp32 torch conv (plain,
+    +residual, masked residual, BN statistics partials) and against the register-staged kernel
+    for the BatchNorm-backward epilogues (modes 3 and 4, per-segment tables)."""
+    from simclr_amd.ops.conv_hip import fwd_geom
+    torch.manual_seed(11)
+    N, H, W, S = 8, 16, 16, 2
+    x = _bf(torch.randn(N, C, H, W, device=DEV))
+    w = _bf(torch.randn(Co, C, k, k, device=DEV) / (C * k * k) ** 0.5)
+    ref = F.conv2d(x.float(), w.float(), None, s, p)
+    OH, OW = ref.shape[-2:]
+    M = N * OH * OW
+    g = fwd_geom(N, H, W, C, OH, OW, k, k, s, p, Co)
+    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    wo = w.permute(0, 2, 3, 1).contiguous()
+    refn = ref.permute(0, 2, 3, 1)
+    r = _bf(torch.randn(N, OH, OW, Co, device=DEV))
+    yy = _bf(torch.randn(N, OH, OW, Co, device=DEV))
+    xa = _bf(torch.randn(N, OH, OW, Co, device=DEV))
+    mi = torch.cat([torch.randn(S, Co, device=DEV) * 0.2,
+                    torch.rand(S, Co, device=DEV) + 0.5]).reshape(-1).contiguous()
+    ss = torch.cat([torch.rand(S, Co, device=DEV) + 0.5,
+                    torch.randn(S, Co, device=DEV) * 0.3]).reshape(-1).contiguous()
+    seg = M // S
+    vs = _glds_variants(ops)
+    assert vs
+    base_v = 0
+
+    def run(v, mode, stats=False, **kw):
+        bm = ops.igemm_variant_bm(v)
+        out = torch.empty(N, OH, OW, Co, device=DEV, dtype=torch.bfloat16)
+        st = torch.empty((M // bm) * 2 * Co, device=DEV) if stats else None
+        ea = kw.get("ea")
+        eb = kw.get("eb")
+        ops.igemm(xn, wo, out, None, st, g, None, None, 0, False, mode, ea, eb, v,
+                  kw.get("ess"), kw.get("emi"), seg if mode >= 3 else 0, 0, 0, kw.get("ec"),
+                  None, None, None, None, None, None)
+        return out, (st.view(M // bm, 2, Co).sum(0) if stats else None)
+
+    for v in vs:
+        if seg % ops.igemm_variant_bm(v):
+            continue
+        out, st = run(v, 0, stats=True)
+        assert _rel(out, refn) < 1e-2, v
+        of = out.float().reshape(-1, Co)
+        assert _rel(st[0], of.sum(0)) < 1e-3 and _rel(st[1], (of * of).sum(0)) < 1e-3, v
+        out, _ = run(v, 1, ea=r)
+        assert _rel(out, refn + r.float()) < 1e-2, v
+        out, _ = run(v, 2, ea=r, eb=yy)
+        assert _rel(out, refn + torch.where(yy.float() > 0, r.float(), 0.0)) < 1e-2, v
+        for mode, kw in ((3, dict(eb=yy, ess=ss, emi=mi)), (4, dict(ea=r, eb=yy, ec=xa, emi=mi))):
+            out, st = run(v, mode, stats=True, **kw)
+            o0, s0 = run(base_v, mode, stats=True, **kw)
+            assert _rel(out, o0) < 1e-2, (v, mode)
+            assert _rel(st, s0) < 1e-3, (v, mode)
+
+
+def test_igemm_glds_dgrad_parity_classes(ops):
+    """Stride-2 dgrad parity-class geometry (negative tap step, strided output rows) on the
+    LDS-DMA kernel against the register-staged kernel, which the conv tests pin to torch."""
+    torch.manual_seed(5)
+    N, H, W, Ci, Co, KH = 4, 16, 16, 64, 128, 3
+    OH, OW, pad = 8, 8, 1
+    dyn = _bf(torch.randn(N, OH, OW, Co, device=DEV))
+    wo = _bf(torch.randn(Co, KH, KH, Ci, device=DEV) * 0.05)
+    for r in (0, 1):
+        for c in (0, 1):
+            kh0, kw0 = (r + pad) % 2, (c + pad) % 2
+            nkh, nkw = (KH - kh0 + 1) // 2, (KH - kw0 + 1) // 2
+            ohc, owc = (H - r + 1) // 2, (W - c + 1) // 2
+            wt = torch.empty((Ci, nkh, nkw, Co), device=DEV, dtype=torch.bfloat16)
+            ops.weight_transform(wo, wt, [Co, KH, KH, Ci, nkh, nkw, kh0, 2, kw0, 2])
+            g = [N, OH, OW, Co, ohc, owc, nkh, nkw, 1, 1, -1, -1, (r + pad - kh0) // 2,
+                 (c + pad - kw0) // 2, Ci, H, W, 2, 2, r, c, Ci]
+            outs = []
+            for v in [0] + _glds_variants(ops):
+                o = torch.zeros(N, H, W, Ci, device=DEV, dtype=torch.bfloat16)
+                ops.igemm(dyn, wt, o, None, None, g, None, None, 0, False, 0, None, None, v)
+                outs.append(o)
+            for v, o in zip(_glds_variants(ops), outs[1:]):
+                assert torch.equal(o, outs[0]) or _rel(o, outs[0]) < 1e-2, (r, c, v)
