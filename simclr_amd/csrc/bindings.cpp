@@ -193,6 +193,7 @@ int64_t igemm_vbm(int64_t v) { return igemm_variant_bm((int)v); }
 int64_t igemm_vbn(int64_t v) { return igemm_variant_bn((int)v); }
 bool igemm_vglds(int64_t v) { return igemm_variant_glds((int)v); }
 int64_t wgrad_nvariants() { return wgrad_num_variants(); }
+bool wgrad_vglds(int64_t v) { return wgrad_variant_glds((int)v); }
 
 int64_t wgrad_nsplit(std::vector<int64_t> gv, int64_t variant) {
   return wgrad_splits(geom_from(gv), (int)variant);
@@ -213,6 +214,10 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
   TORCH_CHECK(out.numel() == (int64_t)g.N * g.KH * g.KW * creal, "wgrad: out numel mismatch");
   TORCH_CHECK(creal <= g.C && creal > 0, "wgrad: bad creal");
   TORCH_CHECK(pro_S >= 1 && pro_S <= 2, "wgrad prologue supports at most 2 segments");
+  if (wgrad_variant_glds((int)variant))
+    TORCH_CHECK(g.C % 64 == 0 && !(pro_sc.has_value() && pro_sc->defined()) &&
+                    !(dY2.has_value() && dY2->defined()),
+                "wgrad: LDS-DMA variant needs C % 64 == 0 and no operand prologue");
   ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, pro_S, 0, c10::nullopt,
                              c10::nullopt, g.C, 0);
   if (f.pro_sc) {
@@ -650,6 +655,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_variant_bn(int v) -> int", &igemm_vbn);
   m.def("igemm_variant_glds(int v) -> bool", &igemm_vglds);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
+  m.def("wgrad_variant_glds(int v) -> bool", &wgrad_vglds);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);

@@ -163,88 +163,108 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
       }
     }
   }
-  for (int row = r0; row < BM; row += RSTEP) {
-    const int m = m0 + row;
-    if (m >= p.M || n >= p.N) continue;
-    u32x4 v = *(const u32x4*)(Cs + row * CST + ch * 8);
-    size_t o;
-    if (p.direct_out) {
-      o = (size_t)m * p.ldo + n;
-    } else {
-      const int img = m / OHW;
-      const int rem = m - img * OHW;
-      const int oh = rem / p.OW;
-      const int ow = rem - oh * p.OW;
-      o = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
-    }
-    if (EPI == 1) {
-      const u32x4 r = *(const u32x4*)(p.epi_a + o);
+  // rows in batches of UNR with every global operand load of the batch issued before any is
+  // consumed: one row at a time left ~1 load set in flight per wave and ran at ~3.5 TB/s
+  constexpr int NIT = BM / RSTEP;
+  constexpr int UNR = NIT < 4 ? NIT : 4;
+  static_assert(NIT % UNR == 0, "epilogue batches");
+  constexpr bool EA = EPI == 1 || EPI == 2 || EPI == 4 || EPI == 5;
+  constexpr bool EB = EPI == 2 || EPI == 3;
+  constexpr bool EC = EPI == 4 || EPI == 5;
+  for (int it0 = 0; it0 < NIT; it0 += UNR) {
+    size_t o[UNR];
+    bool ok[UNR];
+    u32x4 v[UNR], ea[UNR], eb[UNR], ec[UNR], ec2[UNR];
+    unsigned bits[UNR];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        v[e] = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
-    } else if (EPI == 2) {
-      const u32x4 d = *(const u32x4*)(p.epi_a + o);
-      const u32x4 y = *(const u32x4*)(p.epi_b + o);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = lo_bf(y[e]) > 0.f ? lo_bf(d[e]) : 0.f;
-        const float b = hi_bf(y[e]) > 0.f ? hi_bf(d[e]) : 0.f;
-        v[e] = pack2bf(lo_bf(v[e]) + a, hi_bf(v[e]) + b);
+    for (int u = 0; u < UNR; ++u) {
+      const int row = r0 + (it0 + u) * RSTEP;
+      const int m = m0 + row;
+      ok[u] = m < p.M && n < p.N;
+      size_t oo;
+      if (p.direct_out) {
+        oo = (size_t)m * p.ldo + n;
+      } else {
+        const int img = m / OHW;
+        const int rem = m - img * OHW;
+        const int oh = rem / p.OW;
+        const int ow = rem - oh * p.OW;
+        oo = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
       }
-    } else if (EPI == 3) {
-      const u32x4 y = *(const u32x4*)(p.epi_b + o);
+      o[u] = ok[u] ? oo : 0;  // a dead lane reads element 0 and stores nothing
+      v[u] = *(const u32x4*)(Cs + row * CST + ch * 8);
+      if (EA) ea[u] = *(const u32x4*)(p.epi_a + o[u]);
+      if (EC) ec[u] = *(const u32x4*)(p.epi_c + o[u]);
+      if (two) ec2[u] = *(const u32x4*)(p.epi_c2 + o[u]);
+      if (EB) {
+        eb[u] = *(const u32x4*)(p.epi_b + o[u]);
+      } else if (EC) {
+        if (p.epi_mask != nullptr) {
+          bits[u] = p.epi_mask[o[u] >> 3];
+        } else {
+          const u32x4 y = *(const u32x4*)(p.epi_b + o[u]);
+          unsigned b = 0;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float y0 = lo_bf(y[e]), y1 = hi_bf(y[e]);
-        const float g0 = y0 * esc[2 * e] + esh[2 * e] > 0.f ? lo_bf(v[e]) : 0.f;
-        const float g1 = y1 * esc[2 * e + 1] + esh[2 * e + 1] > 0.f ? hi_bf(v[e]) : 0.f;
-        v[e] = pack2bf(g0, g1);  // exact: g is 0 or an already-rounded bf16 value
-        if (p.stats != nullptr) {
-          s1[2 * e] += g0; s2[2 * e] += g0 * ((y0 - emu[2 * e]) * einv[2 * e]);
-          s1[2 * e + 1] += g1; s2[2 * e + 1] += g1 * ((y1 - emu[2 * e + 1]) * einv[2 * e + 1]);
+          for (int e = 0; e < 4; ++e)
+            b |= (lo_bf(y[e]) > 0.f ? 1u : 0u) << (2 * e) | (hi_bf(y[e]) > 0.f ? 2u : 0u) << (2 * e);
+          bits[u] = b;
         }
       }
-    } else if (EPI == 4 || EPI == 5) {
-      const u32x4 r = *(const u32x4*)(p.epi_a + o);
-      const u32x4 xa = *(const u32x4*)(p.epi_c + o);
-      unsigned bits = 0;
-      if (p.epi_mask != nullptr) {
-        bits = p.epi_mask[o >> 3];
-      } else {
-        const u32x4 y = *(const u32x4*)(p.epi_b + o);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (!ok[u]) continue;
+      u32x4 w = v[u];
+      if (EPI == 1) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          bits |= (lo_bf(y[e]) > 0.f ? 1u : 0u) << (2 * e) | (hi_bf(y[e]) > 0.f ? 2u : 0u) << (2 * e);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t sum = pack2bf(lo_bf(v[e]) + lo_bf(r[e]), hi_bf(v[e]) + hi_bf(r[e]));
-        const float g0 = (bits >> (2 * e)) & 1u ? lo_bf(sum) : 0.f;
-        const float g1 = (bits >> (2 * e + 1)) & 1u ? hi_bf(sum) : 0.f;
-        v[e] = pack2bf(g0, g1);
-        if (p.stats != nullptr) {
-          s1[2 * e] += g0; s2[2 * e] += g0 * ((lo_bf(xa[e]) - emu[2 * e]) * einv[2 * e]);
-          s1[2 * e + 1] += g1;
-          s2[2 * e + 1] += g1 * ((hi_bf(xa[e]) - emu[2 * e + 1]) * einv[2 * e + 1]);
-        }
-      }
-      if (two) {
-        const u32x4 xd = *(const u32x4*)(p.epi_c2 + o);
+          w[e] = pack2bf(lo_bf(w[e]) + lo_bf(ea[u][e]), hi_bf(w[e]) + hi_bf(ea[u][e]));
+      } else if (EPI == 2) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float g0 = lo_bf(v[e]), g1 = hi_bf(v[e]);
-          s3[2 * e] += g0 * ((lo_bf(xd[e]) - emu2[2 * e]) * einv2[2 * e]);
-          s3[2 * e + 1] += g1 * ((hi_bf(xd[e]) - emu2[2 * e + 1]) * einv2[2 * e + 1]);
+          const float a = lo_bf(eb[u][e]) > 0.f ? lo_bf(ea[u][e]) : 0.f;
+          const float b = hi_bf(eb[u][e]) > 0.f ? hi_bf(ea[u][e]) : 0.f;
+          w[e] = pack2bf(lo_bf(w[e]) + a, hi_bf(w[e]) + b);
+        }
+      } else if (EPI == 3) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float y0 = lo_bf(eb[u][e]), y1 = hi_bf(eb[u][e]);
+          const float g0 = y0 * esc[2 * e] + esh[2 * e] > 0.f ? lo_bf(w[e]) : 0.f;
+          const float g1 = y1 * esc[2 * e + 1] + esh[2 * e + 1] > 0.f ? hi_bf(w[e]) : 0.f;
+          w[e] = pack2bf(g0, g1);  // exact: g is 0 or an already-rounded bf16 value
+          if (p.stats != nullptr) {
+            s1[2 * e] += g0; s2[2 * e] += g0 * ((y0 - emu[2 * e]) * einv[2 * e]);
+            s1[2 * e + 1] += g1; s2[2 * e + 1] += g1 * ((y1 - emu[2 * e + 1]) * einv[2 * e + 1]);
+          }
+        }
+      } else if (EPI == 4 || EPI == 5) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t sum =
+              pack2bf(lo_bf(w[e]) + lo_bf(ea[u][e]), hi_bf(w[e]) + hi_bf(ea[u][e]));
+          const float g0 = (bits[u] >> (2 * e)) & 1u ? lo_bf(sum) : 0.f;
+          const float g1 = (bits[u] >> (2 * e + 1)) & 1u ? hi_bf(sum) : 0.f;
+          w[e] = pack2bf(g0, g1);
+          if (p.stats != nullptr) {
+            s1[2 * e] += g0; s2[2 * e] += g0 * ((lo_bf(ec[u][e]) - emu[2 * e]) * einv[2 * e]);
+            s1[2 * e + 1] += g1;
+            s2[2 * e + 1] += g1 * ((hi_bf(ec[u][e]) - emu[2 * e + 1]) * einv[2 * e + 1]);
+          }
+          if (two) {
+            s3[2 * e] += g0 * ((lo_bf(ec2[u][e]) - emu2[2 * e]) * einv2[2 * e]);
+            s3[2 * e + 1] += g1 * ((hi_bf(ec2[u][e]) - emu2[2 * e + 1]) * einv2[2 * e + 1]);
+          }
         }
       }
-    }
-    *(u32x4*)(p.out + o) = v;
-    if (EPI < 3 && p.stats != nullptr) {
+      *(u32x4*)(p.out + o[u]) = w;
+      if (EPI < 3 && p.stats != nullptr) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = lo_bf(v[e]), b = hi_bf(v[e]);
-        s1[2 * e] += a; s2[2 * e] += a * a;
-        s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
+        for (int e = 0; e < 4; ++e) {
+          const float a = lo_bf(w[e]), b = hi_bf(w[e]);
+          s1[2 * e] += a; s2[2 * e] += a * a;
+          s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
+        }
       }
     }
   }
@@ -599,6 +619,74 @@ struct WgradArgs {
   int dp_seg_rows, dp_S;
 };
 
+// One 64-deep step of the weight-gradient tile from swizzled row-major LDS images (rows = m):
+// both MFMA operands are read transposed with ds_read_b64_tr_b16.
+template <int BCO, int BKK, int WM, int WN>
+__device__ __forceinline__ void wgrad_mma(const uint16_t* Db, const uint16_t* Xb,
+                                          f32x4 (&acc)[BCO / WM / 16][BKK / WN / 16]) {
+  constexpr int TCO = BCO / WM, TKK = BKK / WN;
+  constexpr int FM = TCO / 16, FN = TKK / 16;
+  constexpr int SD = BCO, SX = BKK;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int r1 = ks * 32 + 8 * g + q;
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int col = wm * TCO + fm * 16 + 4 * pp;
+      i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Db + r1 * SD + tr_swz<BCO>(r1, col)));
+      i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Db + (r1 + 4) * SD + tr_swz<BCO>(r1 + 4, col)));
+      i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[fm] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int col = wn * TKK + fn * 16 + 4 * pp;
+      i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Xb + r1 * SX + tr_swz<BKK>(r1, col)));
+      i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Xb + (r1 + 4) * SX + tr_swz<BKK>(r1 + 4, col)));
+      i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[fn] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+        acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+  }
+}
+
+// fp32 partial slab of one split: partial[split][co][k]
+template <int BCO, int BKK, int WM, int WN>
+__device__ __forceinline__ void wgrad_store(const WgradArgs& p,
+                                            f32x4 (&acc)[BCO / WM / 16][BKK / WN / 16],
+                                            int split, int co0, int k0) {
+  constexpr int TCO = BCO / WM, TKK = BKK / WN;
+  constexpr int FM = TCO / 16, FN = TKK / 16;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int g = lane >> 4, li = lane & 15;
+  float* out = p.partial + (size_t)split * p.N * p.K;
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int kcol = k0 + wn * TKK + fn * 16 + li;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co0 + wm * TCO + fm * 16 + g * 4 + i;
+        if (co < p.N && kcol < p.K) out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
+      }
+    }
+}
+
 template <int BCO, int BKK, int WM, int WN, bool PRO, bool DPRO>
 __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn(WgradArgs p) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
@@ -756,7 +844,6 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   if (nit > 0) {
     gload(0);
     lstore(0);
@@ -765,55 +852,124 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
   for (int it = 0; it < nit; ++it) {
     const int cur = it & 1;
     if (it + 1 < nit) gload(it + 1);
-    const uint16_t* Db = Ds + cur * 64 * SD;
-    const uint16_t* Xb = Xs + cur * 64 * SX;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int r1 = ks * 32 + 8 * g + q;
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const int col = wm * TCO + fm * 16 + 4 * pp;
-        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, Db + r1 * SD + tr_swz<BCO>(r1, col)));
-        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, Db + (r1 + 4) * SD + tr_swz<BCO>(r1 + 4, col)));
-        typedef short i16x8 __attribute__((ext_vector_type(8)));
-        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[fm] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int col = wn * TKK + fn * 16 + 4 * pp;
-        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, Xb + r1 * SX + tr_swz<BKK>(r1, col)));
-        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, Xb + (r1 + 4) * SX + tr_swz<BKK>(r1 + 4, col)));
-        typedef short i16x8 __attribute__((ext_vector_type(8)));
-        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[fn] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
-    }
+    wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * SD, Xs + cur * 64 * SX, acc);
     if (it + 1 < nit) lstore(cur ^ 1);
     __syncthreads();
   }
-  float* out = p.partial + (size_t)split * p.N * p.K;
+  wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
+}
+
+// Weight gradient with LDS-DMA staging (no operand prologue; C % 64 == 0): the dY and im2col(X)
+// row tiles are DMA'd into the same swizzled row-major images wgrad_tn builds (each lane fetches
+// the logical chunk tr_swz maps onto its lane-linear LDS slot), then read transposed by
+// ds_read_b64_tr_b16.  Each block's (co0, k0) window is fixed, so every lane's X column (tap,
+// channel) is constant and only its output pixel advances by 64 rows per step.
+template <int BCO, int BKK, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
+  constexpr int NW = WM * WN;
+  constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = 64 / (RPD * NW);
+  constexpr int CPX = BKK / 8, RPX = 64 / CPX, XI = 64 / (RPX * NW);
+  static_assert(DI >= 1 && XI >= 1 && DI * RPD * NW == 64 && XI * RPX * NW == 64, "wgrad glds");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ds = (uint16_t*)smem;   // [2][64][BCO]
+  uint16_t* Xs = Ds + 2 * 64 * BCO;  // [2][64][BKK]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = p.nCo * p.nKk;
+  const int split = lbid / tiles;
+  const int tile = lbid % tiles;
+  const int co0 = (tile / p.nKk) * BCO;
+  const int k0 = (tile % p.nKk) * BKK;
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, (int)p.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
+  const int mbeg = split * p.iters_per_split * 64;
+  const int mend_raw = mbeg + p.iters_per_split * 64;
+  const int mend = mend_raw < p.M ? mend_raw : p.M;
+  const int nit = mend > mbeg ? (mend - mbeg + 63) / 64 : 0;
+  const int OHW = p.OH * p.OW;
+
+  // dY: lane → (row in piece, physical chunk) → logical column chunk
+  int d_row[DI];
+  uint32_t d_off[DI];
+  bool d_cok[DI];
 #pragma unroll
-  for (int fm = 0; fm < FM; ++fm)
+  for (int j = 0; j < DI; ++j) {
+    const int r = (j * NW + wid) * RPD + lane / CPD;
+    const int col = co0 + tr_swz<BCO>(r, (lane % CPD) * 8);
+    d_row[j] = r;
+    d_cok[j] = col < p.N;
+    d_off[j] = (uint32_t)(((size_t)(mbeg + r) * p.N + col) * 2);
+  }
+  const uint32_t dstep = (uint32_t)(64 * p.N * 2);
+  // X: fixed (tap, channel) per lane and piece; output pixel carried incrementally
+  int x_row[XI], x_ci[XI], x_ihb[XI], x_iwb[XI], xn[XI], xoh[XI], xow[XI];
+  bool x_kok[XI];
 #pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int kcol = k0 + wn * TKK + fn * 16 + li;
+  for (int j = 0; j < XI; ++j) {
+    const int r = (j * NW + wid) * RPX + lane / CPX;
+    const int kk = k0 + tr_swz<BKK>(r, (lane % CPX) * 8);
+    x_row[j] = r;
+    x_kok[j] = kk < p.K;
+    const int tap = x_kok[j] ? kk / p.C : 0;
+    x_ci[j] = kk - tap * p.C;
+    const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+    x_ihb[j] = p.ih0 + kh * p.dh;
+    x_iwb[j] = p.iw0 + kw * p.dw;
+    const int m = mbeg + r;
+    xn[j] = m / OHW;
+    const int rem = m - xn[j] * OHW;
+    xoh[j] = rem / p.OW;
+    xow[j] = rem - xoh[j] * p.OW;
+  }
+  const int dn = 64 / OHW, dr = 64 - dn * OHW;
+  const int doh = dr / p.OW, dow = dr - doh * p.OW;
+  const int cstride = p.C * 2;
+
+  auto issue = [&](int it, int buf) {
+    const int mb = mbeg + it * 64;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int co = co0 + wm * TCO + fm * 16 + g * 4 + i;
-        if (co < p.N && kcol < p.K) out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
-      }
+    for (int j = 0; j < DI; ++j) {
+      const bool ok = mb + d_row[j] < mend && d_cok[j];
+      dma16(rd, Ds + buf * 64 * BCO + (j * NW + wid) * RPD * BCO, ok ? d_off[j] : p.dy_bytes);
+      d_off[j] += dstep;
     }
+#pragma unroll
+    for (int j = 0; j < XI; ++j) {
+      const int ih = (int)__umul24((unsigned)xoh[j], (unsigned)p.ish) + x_ihb[j];
+      const int iw = (int)__umul24((unsigned)xow[j], (unsigned)p.isw) + x_iwb[j];
+      const bool ok = mb + x_row[j] < mend && x_kok[j] && (unsigned)ih < (unsigned)p.IH &&
+                      (unsigned)iw < (unsigned)p.IW;
+      const uint32_t pix =
+          __umul24(__umul24((unsigned)xn[j], (unsigned)p.IH) + (unsigned)ih, (unsigned)p.IW) +
+          (unsigned)iw;
+      const uint32_t off = ok ? __umul24(pix, (unsigned)cstride) + (uint32_t)(x_ci[j] * 2)
+                              : p.x_bytes;
+      dma16(rx, Xs + buf * 64 * BKK + (j * NW + wid) * RPX * BKK, off);
+      int ow = xow[j] + dow, oh = xoh[j] + doh, n = xn[j] + dn;
+      if (ow >= p.OW) { ow -= p.OW; ++oh; }
+      if (oh >= p.OH) { oh -= p.OH; ++n; }
+      xow[j] = ow; xoh[j] = oh; xn[j] = n;
+    }
+  };
+
+  f32x4 acc[BCO / WM / 16][BKK / WN / 16];
+#pragma unroll
+  for (int i = 0; i < BCO / WM / 16; ++i)
+#pragma unroll
+    for (int j = 0; j < BKK / WN / 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (nit > 0) issue(0, 0);
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (it + 1 < nit) issue(it + 1, cur ^ 1);
+    wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * BCO, Xs + cur * 64 * BKK, acc);
+  }
+  wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
 }
 
 // out[co][tap][ci < Creal] (+)= Σ_s partial[s*stride][co][tap*C + ci]   (slab stride in slabs)
@@ -1028,6 +1184,17 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+template <int BCO, int BKK, int WM, int WN>
+void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
+  WgradArgs a = a0;
+  a.nCo = (a.N + BCO - 1) / BCO;
+  a.nKk = (a.K + BKK - 1) / BKK;
+  const int grid = a.nCo * a.nKk * a.splits;
+  const size_t lds = (size_t)2 * 64 * (BCO + BKK) * 2;
+  hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
 // tile variants: {BM, BN}
 // wide-N / wide-K tiles (5, 6 and wgrad 4, 5) cover a whole small output dimension in one tile,
 // so the other operand is streamed from HBM once instead of N/BN (K/BKK) times
@@ -1036,7 +1203,15 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
                                   {128, 256}, {64, 256},
                                   {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256}};
 constexpr int IG_GLDS0 = 7;
-constexpr int WG_VARIANTS[][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {64, 256}, {256, 64}};
+// variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
+// {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
+// that many blocks; every split costs an fp32 N x K slab written here and re-read by the
+// reduction, so the LDS-DMA variants (1-2 blocks per CU) aim at 256-512 instead of 768
+constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768}, {64, 64, 768},
+                                  {64, 256, 768},  {256, 64, 768},  {128, 128, 512},
+                                  {256, 128, 256}, {128, 256, 256}, {256, 256, 256},
+                                  {64, 256, 512},  {128, 128, 256}, {64, 256, 256}};
+constexpr int WG_GLDS0 = 6;
 
 }  // namespace
 
@@ -1098,6 +1273,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
 
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
+bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < wgrad_num_variants(); }
 
 int wgrad_splits(const ConvGeom& g, int variant) {
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
@@ -1106,7 +1282,8 @@ int wgrad_splits(const ConvGeom& g, int variant) {
   const int K = g.KH * g.KW * g.C;
   const int tiles = ((g.N + bco - 1) / bco) * ((K + bkk - 1) / bkk);
   const int iters = (M + 63) / 64;
-  int splits = (768 + tiles - 1) / tiles;
+  const int target = WG_VARIANTS[variant][2];
+  int splits = (target + tiles - 1) / tiles;
   int max_splits = iters / 8;
   if (max_splits < 1) max_splits = 1;
   if (splits > max_splits) splits = max_splits;
@@ -1134,7 +1311,20 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.dY2 = f.dY2; a.dp_coef = f.dp_coef; a.dp_seg_rows = f.dp_seg_rows > 0 ? f.dp_seg_rows : a.M;
   a.dp_S = f.dp_S > 0 ? f.dp_S : 1;
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
+  if (wgrad_variant_glds(variant) && (a.pro_sc != nullptr || a.dY2 != nullptr || g.C % 64 != 0)) {
+    fprintf(stderr, "wgrad: LDS-DMA variant %d needs C %% 64 == 0 and no prologue\n", variant);
+    abort();  // the bindings reject this
+  }
   switch (variant) {
+    // 4-wave tiles with 128x64 / 64x128 per wave: half the LDS fragment bytes per MFMA of a
+    // 64x64 wave tile (the 128x128 wgrad was LDS-bound between DMA writes and tr reads)
+    case 6: launch_wgrad_glds<128, 128, 2, 2>(a, s); break;
+    case 7: launch_wgrad_glds<256, 128, 2, 2>(a, s); break;
+    case 8: launch_wgrad_glds<128, 256, 2, 2>(a, s); break;
+    case 9: launch_wgrad_glds<256, 256, 2, 4>(a, s); break;
+    case 10: launch_wgrad_glds<64, 256, 1, 4>(a, s); break;
+    case 11: launch_wgrad_glds<128, 128, 2, 2>(a, s); break;
+    case 12: launch_wgrad_glds<64, 256, 1, 4>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;

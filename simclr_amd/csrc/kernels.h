@@ -57,6 +57,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
                    int variant, hipStream_t s);
 int wgrad_num_variants();
 int wgrad_default_variant(int N);
+bool wgrad_variant_glds(int v);  // LDS-DMA variant: no prologues, needs C % 64 == 0
 int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
                 float* partial, int splits, float* out, int Creal, float beta,

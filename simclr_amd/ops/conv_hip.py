@@ -138,7 +138,10 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
         ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v,
                   dY2, dcoef, dseg, dS)
 
-    v = tuning.pick(key, range(ops.wgrad_nvariants()), 1 if N <= 64 else 0,
+    cands = [v for v in range(ops.wgrad_nvariants())
+             if not (ops.wgrad_variant_glds(v) and (psc is not None or dpro is not None
+                                                    or geom[3] % 64))]
+    v = tuning.pick(key, cands, 1 if N <= 64 else 0,
                     lambda vv: launch(vv, torch.empty_like(out)))
     launch(v, out)
 

@@ -284,6 +284,8 @@ def test_igemm_variants_prologue_epilogue(ops, k, s, p):
     yref.backward(gy.float())
     dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
     for v in range(ops.wgrad_nvariants()):
+        if ops.wgrad_variant_glds(v):
+            continue
         splits = ops.wgrad_splits(g, v)
         K = k * k * C
         part = torch.empty(splits * Co * K, device=DEV)
@@ -379,3 +381,33 @@ def test_igemm_glds_dgrad_parity_classes(ops):
                 outs.append(o)
             for v, o in zip(_glds_variants(ops), outs[1:]):
                 assert torch.equal(o, outs[0]) or _rel(o, outs[0]) < 1e-2, (r, c, v)
+
+
+@pytest.mark.parametrize("k,s,p,C,Co,H", [(1, 1, 0, 64, 256, 16), (3, 1, 1, 64, 64, 16),
+                                           (3, 2, 1, 128, 192, 16), (1, 2, 0, 128, 128, 16),
+                                           (3, 1, 1, 256, 512, 4), (3, 1, 1, 64, 64, 5)])
+def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
+    """LDS-DMA weight gradient (wgrad_glds), every tile variant and a few split counts, against
+    torch's fp32 conv2d weight gradient (partial M tiles: H=5 gives M % 64 != 0)."""
+    from simclr_amd.ops.conv_hip import fwd_geom
+    torch.manual_seed(13)
+    N = 8
+    x = _bf(torch.randn(N, C, H, H, device=DEV))
+    wr = (_bf(torch.randn(Co, C, k, k, device=DEV)) * 0.05).float().requires_grad_(True)
+    y = F.conv2d(x.float(), wr, None, s, p)
+    gy = _bf(torch.randn_like(y))
+    y.backward(gy.float())
+    OH, OW = y.shape[-2:]
+    g = fwd_geom(N, H, H, C, OH, OW, k, k, s, p, Co)
+    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    K = k * k * C
+    vs = [v for v in range(ops.wgrad_nvariants()) if ops.wgrad_variant_glds(v)]
+    assert vs
+    for v in vs:
+        base = ops.wgrad_splits(g, v)
+        for splits in sorted({1, 3, base}):
+            part = torch.empty(splits * Co * K, device=DEV)
+            out = torch.empty(Co, k, k, C, device=DEV)
+            ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, None, None, 0, False, 1, v)
+            assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)

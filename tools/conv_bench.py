@@ -91,6 +91,8 @@ def main():
         dyn = torch.randn(N, OH, OW, Co, device=dev).to(torch.bfloat16)
         out = torch.empty(Co, k, k, Cg, device=dev)
         for v in range(ops.wgrad_nvariants()):
+            if ops.wgrad_variant_glds(v) and Cg % 64:
+                continue
             sp = ops.wgrad_splits(g, v)
             part = torch.empty(sp * Co * k * k * Cg, device=dev)
             wg[v] = timeit(lambda: ops.wgrad(dyn, x, part, out, g, sp, Cg, 0.0, None, None, 0,
@@ -111,8 +113,8 @@ def main():
               f"{row['fwd_gbs']:6.0f} GB/s) v={min(fw, key=fw.get)} "
               f"| dgrad {dg or 0:7.1f}us | wgrad best {bw:7.1f}us ({row['wgrad_tflops']:6.1f} TF)"
               f" v={min(wg, key=wg.get)}", flush=True)
-        print("    fwd us by variant: " + " ".join(f"{v}:{t:.0f}" for v, t in fw.items()),
-              flush=True)
+        print("    fwd us by variant: " + " ".join(f"{v}:{t:.0f}" for v, t in fw.items()) +
+              " | wgrad: " + " ".join(f"{v}:{t:.0f}" for v, t in wg.items()), flush=True)
     print("totals (us, x count):", {k: round(v, 1) for k, v in tot_best.items()})
     if a.json:
         Path(a.json).write_text(json.dumps({"rows": rows, "totals_us": tot_best}, indent=1,
