@@ -118,8 +118,10 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int bm = igemm_variant_bm((int)variant);
   if (igemm_variant_glds((int)variant))
-    TORCH_CHECK(g.C % 64 == 0 && !(pro_sc.has_value() && pro_sc->defined()),
-                "igemm: LDS-DMA variant needs C % 64 == 0 and no operand prologue");
+    TORCH_CHECK(igemm_glds_ok(g, pro_sc.has_value() && pro_sc->defined(),
+                              pro_d.has_value() && pro_d->defined()),
+                "igemm: LDS-DMA variant needs C % 64 == 0, no BN-backward prologue, and a BN-apply "
+                "prologue only on unpadded 1x1 convolutions");
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
   const bool has_stats = stats.has_value() && stats->defined();
   if (has_stats && stats_seg_blocks == 0)
@@ -192,6 +194,9 @@ int64_t igemm_nvariants() { return igemm_num_variants(); }
 int64_t igemm_vbm(int64_t v) { return igemm_variant_bm((int)v); }
 int64_t igemm_vbn(int64_t v) { return igemm_variant_bn((int)v); }
 bool igemm_vglds(int64_t v) { return igemm_variant_glds((int)v); }
+bool igemm_gldsok(std::vector<int64_t> gv, bool pro, bool bn_bwd_pro) {
+  return igemm_glds_ok(geom_from(gv), pro, bn_bwd_pro);
+}
 int64_t wgrad_nvariants() { return wgrad_num_variants(); }
 bool wgrad_vglds(int64_t v) { return wgrad_variant_glds((int)v); }
 
@@ -654,6 +659,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);
   m.def("igemm_variant_bn(int v) -> int", &igemm_vbn);
   m.def("igemm_variant_glds(int v) -> bool", &igemm_vglds);
+  m.def("igemm_glds_ok(int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_gldsok);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
   m.def("wgrad_variant_glds(int v) -> bool", &wgrad_vglds);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);

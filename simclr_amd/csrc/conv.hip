@@ -269,19 +269,34 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
     }
   }
   if (p.stats != nullptr) {
-    __syncthreads();
+    // lanes of a wave that share a column chunk (tid % CPR) sum their rows with cross-lane
+    // xor-shuffles first; only one partial per wave goes through LDS
     constexpr int NS = two ? 3 : 2;
-    float* red = (float*)smem;  // [RSTEP][BN][NS]
+    constexpr int NWV = NT / 64;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(r0 * BN + ch * 8 + e) * NS + 0] = s1[e];
-      red[(r0 * BN + ch * 8 + e) * NS + 1] = s2[e];
-      if (two) red[(r0 * BN + ch * 8 + e) * NS + 2] = s3[e];
+    for (int off = CPR; off < 64; off <<= 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += __shfl_xor(s1[e], off, 64);
+        s2[e] += __shfl_xor(s2[e], off, 64);
+        if (two) s3[e] += __shfl_xor(s3[e], off, 64);
+      }
+    }
+    __syncthreads();
+    float* red = (float*)smem;  // [NWV][BN][NS]
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wid * BN + ch * 8 + e) * NS + 0] = s1[e];
+        red[(wid * BN + ch * 8 + e) * NS + 1] = s2[e];
+        if (two) red[(wid * BN + ch * 8 + e) * NS + 2] = s3[e];
+      }
     }
     __syncthreads();
     if (tid < BN && n0 + tid < p.N) {
       float a = 0.f, b = 0.f, d = 0.f;
-      for (int r = 0; r < RSTEP; ++r) {
+#pragma unroll
+      for (int r = 0; r < NWV; ++r) {
         a += red[(r * BN + tid) * NS + 0];
         b += red[(r * BN + tid) * NS + 1];
         if (two) d += red[(r * BN + tid) * NS + 2];
@@ -478,7 +493,10 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds,
 // Pipeline: 2 LDS stages, BK = 64; the DMA of tile k+1 is issued right after the barrier that
 // publishes tile k and runs under tile k's MFMAs; one vmcnt(0) + barrier per k-tile.
 // Host guarantees: C % 64 == 0 (a 64-wide K slice is one tap), no prologue.
-template <int BM, int BN, int WM, int WN, int EPI>
+// PRO == 1 (1x1 convolutions without padding only, host-checked): the previous BatchNorm's
+// normalise + ReLU is applied to the A tile in LDS after the DMA lands (one read-modify-write
+// pass and one extra barrier per k-tile), so the conv3 forward keeps the DMA pipeline too.
+template <int BM, int BN, int WM, int WN, int PRO, int EPI>
 __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -555,12 +573,29 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / 64;
+  const int pseg = PRO ? m0 / p.pro_seg_rows : 0;  // block-uniform (host guarantees)
   issue(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // tile kt visible to every wave; every wave is done reading buffer cur^1
     if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    if (PRO) {
+      const int ci0 = kt * 64 - (kt * 64 / p.C) * p.C;
+#pragma unroll
+      for (int i = 0; i < BM * 8 / NT; ++i) {
+        const int c = tid + i * NT;
+        const int row = c >> 3, lc = (c & 7) ^ (row & 7);
+        const float4* ps = (const float4*)(p.pro_sc + pseg * p.C + ci0 + lc * 8);
+        const float4* ph = (const float4*)(p.pro_sh + pseg * p.C + ci0 + lc * 8);
+        const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        u32x4* q = (u32x4*)(As + cur * BM * 64 + c * 8);
+        *q = affine_relu8(*q, sc, sh, true, p.pro_relu != 0);
+      }
+      __syncthreads();
+    }
     const uint16_t* Ab = As + cur * BM * 64;
     const uint16_t* Bb = Bs + cur * BN * 64;
 #pragma unroll
@@ -1100,7 +1135,7 @@ void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int PRO, int EPI>
 void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   IgemmArgs a = a0;
   a.nMb = (a.M + BM - 1) / BM;
@@ -1111,23 +1146,33 @@ void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   const size_t red = (size_t)(NT / (BN / 8)) * BN * 3 * 4;
   if (cst > lds) lds = cst;
   if (red > lds) lds = red;
-  hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, EPI>), dim3(a.nMb * a.nNb), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI>), dim3(a.nMb * a.nNb), dim3(NT), lds, s,
+                     a);
   HIP_CHECK_LAUNCH();
 }
 
 template <int BM, int BN, int WM, int WN>
 void launch_glds(const IgemmArgs& a, hipStream_t s) {
+  if (a.pro_sc != nullptr) {
+    switch (a.epi_mode) {
+      case 1: launch_glds_t<BM, BN, WM, WN, 1, 1>(a, s); break;
+      case 2: launch_glds_t<BM, BN, WM, WN, 1, 2>(a, s); break;
+      case 3: launch_glds_t<BM, BN, WM, WN, 1, 3>(a, s); break;
+      default: launch_glds_t<BM, BN, WM, WN, 1, 0>(a, s); break;
+    }
+    return;
+  }
   switch (a.epi_mode) {
-    case 1: launch_glds_t<BM, BN, WM, WN, 1>(a, s); break;
-    case 2: launch_glds_t<BM, BN, WM, WN, 2>(a, s); break;
-    case 3: launch_glds_t<BM, BN, WM, WN, 3>(a, s); break;
+    case 1: launch_glds_t<BM, BN, WM, WN, 0, 1>(a, s); break;
+    case 2: launch_glds_t<BM, BN, WM, WN, 0, 2>(a, s); break;
+    case 3: launch_glds_t<BM, BN, WM, WN, 0, 3>(a, s); break;
     case 4:
       if (a.stats2 != nullptr)
-        launch_glds_t<BM, BN, WM, WN, 5>(a, s);
+        launch_glds_t<BM, BN, WM, WN, 0, 5>(a, s);
       else
-        launch_glds_t<BM, BN, WM, WN, 4>(a, s);
+        launch_glds_t<BM, BN, WM, WN, 0, 4>(a, s);
       break;
-    default: launch_glds_t<BM, BN, WM, WN, 0>(a, s); break;
+    default: launch_glds_t<BM, BN, WM, WN, 0, 0>(a, s); break;
   }
 }
 
@@ -1225,6 +1270,11 @@ int igemm_variant_bm(int v) { return IG_VARIANTS[v][0]; }
 int igemm_variant_bn(int v) { return IG_VARIANTS[v][1]; }
 int igemm_default_variant(int N) { return N <= 64 ? 1 : 0; }
 bool igemm_variant_glds(int v) { return v >= IG_GLDS0 && v < igemm_num_variants(); }
+bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro) {
+  if (g.C % 64 != 0 || bn_bwd_pro) return false;
+  // the BN-apply prologue runs on the landed tile: only valid without zero-padding taps
+  return !pro || (g.KH == 1 && g.KW == 1 && g.ih0 == 0 && g.iw0 == 0);
+}
 int igemm_block_m(int N) { return igemm_variant_bm(igemm_default_variant(N)); }
 
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
@@ -1251,8 +1301,8 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
-  if (igemm_variant_glds(variant) && (a.pro_sc != nullptr || g.C % 64 != 0)) {
-    fprintf(stderr, "igemm: LDS-DMA variant %d needs C %% 64 == 0 and no prologue\n", variant);
+  if (igemm_variant_glds(variant) && !igemm_glds_ok(g, a.pro_sc != nullptr, a.pro_d != nullptr)) {
+    fprintf(stderr, "igemm: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
     abort();  // the bindings reject this; never silently change BM (stats layout)
   }
   switch (variant) {

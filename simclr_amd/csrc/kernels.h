@@ -50,7 +50,8 @@ int igemm_num_variants();
 int igemm_variant_bm(int v);
 int igemm_variant_bn(int v);
 int igemm_default_variant(int N);
-bool igemm_variant_glds(int v);  // LDS-DMA variant: no prologue, needs C % 64 == 0
+bool igemm_variant_glds(int v);  // LDS-DMA variant (see igemm_glds_ok)
+bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro);
 int igemm_block_m(int N);
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
                    uint16_t* out, const float* bias, float* stats, const ConvFusion& f,

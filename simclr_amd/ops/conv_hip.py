@@ -40,8 +40,9 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
     cands = []
     for v in range(ops.igemm_nvariants()):
         bm = ops.igemm_variant_bm(v)
-        if ops.igemm_variant_glds(v) and (psc is not None or geom[3] % 64):
-            continue  # LDS-DMA variants: no operand prologue, C % 64 == 0
+        if ops.igemm_variant_glds(v) and not ops.igemm_glds_ok(geom, psc is not None,
+                                                               bnb is not None):
+            continue  # LDS-DMA variants: C % 64 == 0, BN-apply prologue only on unpadded 1x1
         if want_stats and M % bm:
             continue
         if psc is not None and pseg % bm:
