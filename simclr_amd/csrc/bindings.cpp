@@ -220,9 +220,10 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
   TORCH_CHECK(creal <= g.C && creal > 0, "wgrad: bad creal");
   TORCH_CHECK(pro_S >= 1 && pro_S <= 2, "wgrad prologue supports at most 2 segments");
   if (wgrad_variant_glds((int)variant))
-    TORCH_CHECK(g.C % 64 == 0 && !(pro_sc.has_value() && pro_sc->defined()) &&
-                    !(dY2.has_value() && dY2->defined()),
-                "wgrad: LDS-DMA variant needs C % 64 == 0 and no operand prologue");
+    TORCH_CHECK(igemm_glds_ok(g, pro_sc.has_value() && pro_sc->defined(),
+                              dY2.has_value() && dY2->defined()),
+                "wgrad: LDS-DMA variant needs C % 64 == 0, no dY prologue, and an X prologue only "
+                "on unpadded 1x1 convolutions");
   ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, pro_S, 0, c10::nullopt,
                              c10::nullopt, g.C, 0);
   if (f.pro_sc) {

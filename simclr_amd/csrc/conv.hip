@@ -493,6 +493,18 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds,
 // Pipeline: 2 LDS stages, BK = 64; the DMA of tile k+1 is issued right after the barrier that
 // publishes tile k and runs under tile k's MFMAs; one vmcnt(0) + barrier per k-tile.
 // Host guarantees: C % 64 == 0 (a 64-wide K slice is one tap), no prologue.
+// byte offset of igemm_glds's prologue table: after the larger of the staging buffers, the
+// epilogue's C image and its statistics scratch
+__host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int NT) {
+  return ((size_t)2 * (BM + BN) * 64 * 2 > (size_t)BM * (BN + 8) * 2
+              ? ((size_t)2 * (BM + BN) * 64 * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
+                     ? (size_t)2 * (BM + BN) * 64 * 2
+                     : (size_t)(NT / (BN / 8)) * BN * 3 * 4)
+              : ((size_t)BM * (BN + 8) * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
+                     ? (size_t)BM * (BN + 8) * 2
+                     : (size_t)(NT / (BN / 8)) * BN * 3 * 4));
+}
+
 // PRO == 1 (1x1 convolutions without padding only, host-checked): the previous BatchNorm's
 // normalise + ReLU is applied to the A tile in LDS after the DMA lands (one read-modify-write
 // pass and one extra barrier per k-tile), so the conv3 forward keeps the DMA pipeline too.
@@ -506,6 +518,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* As = (uint16_t*)smem;   // [2][BM][64]
   uint16_t* Bs = As + 2 * BM * 64;  // [2][BN][64]
+  // PRO: [sc, sh][C] of the block's segment, behind the staging buffers and the epilogue image
+  float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN));
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -573,7 +587,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / 64;
-  const int pseg = PRO ? m0 / p.pro_seg_rows : 0;  // block-uniform (host guarantees)
+  if (PRO) {
+    // table staged before any DMA: ordinary global loads consumed in the loop would make hipcc
+    // drain the in-flight DMA (vmcnt(0)) right after it is issued
+    const int pseg = m0 / p.pro_seg_rows;  // block-uniform (host guarantees)
+    for (int i = tid; i < 2 * p.C; i += NT)
+      Pt[i] = (i < p.C ? p.pro_sc : p.pro_sh)[pseg * p.C + (i < p.C ? i : i - p.C)];
+    __syncthreads();
+  }
   issue(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
@@ -586,15 +607,17 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       for (int i = 0; i < BM * 8 / NT; ++i) {
         const int c = tid + i * NT;
         const int row = c >> 3, lc = (c & 7) ^ (row & 7);
-        const float4* ps = (const float4*)(p.pro_sc + pseg * p.C + ci0 + lc * 8);
-        const float4* ph = (const float4*)(p.pro_sh + pseg * p.C + ci0 + lc * 8);
+        const float4* ps = (const float4*)(Pt + ci0 + lc * 8);
+        const float4* ph = (const float4*)(Pt + p.C + ci0 + lc * 8);
         const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
         const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
         const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
         u32x4* q = (u32x4*)(As + cur * BM * 64 + c * 8);
         *q = affine_relu8(*q, sc, sh, true, p.pro_relu != 0);
       }
-      __syncthreads();
+      // raw barrier: __syncthreads() would also drain the next tile's DMA (vmcnt(0))
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
     const uint16_t* Ab = As + cur * BM * 64;
     const uint16_t* Bb = Bs + cur * BN * 64;
@@ -899,7 +922,12 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 // the logical chunk tr_swz maps onto its lane-linear LDS slot), then read transposed by
 // ds_read_b64_tr_b16.  Each block's (co0, k0) window is fixed, so every lane's X column (tap,
 // channel) is constant and only its output pixel advances by 64 rows per step.
-template <int BCO, int BKK, int WM, int WN>
+// PRO (unpadded 1x1 only, host-checked): the X operand's BatchNorm-apply + ReLU runs on the
+// landed LDS tile (per-row segment, per-column channel), one extra barrier per step.
+// NST LDS stages: with NST == 3 the DMA of step it+2 is issued while step it computes and a
+// counted vmcnt keeps step it+1's DMA in flight across the barrier (raw s_barrier: hipcc's
+// __syncthreads() would drain it with vmcnt(0)) — for the HBM-bound 1x1 weight gradients.
+template <int BCO, int BKK, int WM, int WN, bool PRO, int NST>
 __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
   constexpr int NW = WM * WN;
   constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = 64 / (RPD * NW);
@@ -907,7 +935,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
   static_assert(DI >= 1 && XI >= 1 && DI * RPD * NW == 64 && XI * RPX * NW == 64, "wgrad glds");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* Ds = (uint16_t*)smem;   // [2][64][BCO]
-  uint16_t* Xs = Ds + 2 * 64 * BCO;  // [2][64][BKK]
+  uint16_t* Xs = Ds + NST * 64 * BCO;  // [NST][64][BKK]
+  float* Pt = (float*)(Xs + NST * 64 * BKK);  // PRO: [sc, sh][segment 0, 1][BKK] of this k window
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lbid = xcd_remap(blockIdx.x, gridDim.x);
@@ -996,12 +1025,50 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
 #pragma unroll
     for (int j = 0; j < BKK / WN / 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (nit > 0) issue(0, 0);
-  for (int it = 0; it < nit; ++it) {
-    const int cur = it & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  constexpr int PER = DI + XI;  // DMA instructions per wave per step
+  if (PRO) {
+    // the prologue's per-channel table is staged in LDS before any DMA is issued: an ordinary
+    // global load consumed inside the loop would make hipcc drain the DMA queue (vmcnt(0))
+    for (int i = tid; i < 4 * BKK; i += 64 * NW) {
+      const int which = i / (2 * BKK), sg = (i / BKK) & 1, col = i % BKK;
+      const int kk = k0 + col < p.K ? k0 + col : 0;
+      const int sgs = p.pro_S > 1 ? sg : 0;
+      Pt[i] = (which ? p.pro_sh : p.pro_sc)[sgs * p.C + kk];
+    }
     __syncthreads();
-    if (it + 1 < nit) issue(it + 1, cur ^ 1);
+  }
+  if (nit > 0) issue(0, 0);
+  if (NST == 3 && nit > 1) issue(1, 1);
+  for (int it = 0; it < nit; ++it) {
+    const int cur = NST == 3 ? it % 3 : it & 1;
+    if (NST == 3 && it + 1 < nit)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step it+1 stays in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // step it landed for every wave; buffer (it-1) % NST is free
+    if (it + NST - 1 < nit) issue(it + NST - 1, (it + NST - 1) % NST);
+    if (PRO) {
+      // rows past mend hold zero dY, so whatever the transform makes of them contributes 0;
+      // columns past K are dropped by the store
+      const int mb = mbeg + it * 64;
+#pragma unroll
+      for (int i = 0; i < 64 * CPX / (64 * NW); ++i) {
+        const int c = tid + i * 64 * NW;
+        const int row = c / CPX, pc = c % CPX;
+        const int col = tr_swz<BKK>(row, pc * 8);
+        const int sg = (p.pro_S > 1 && mb + row >= p.pro_seg_rows) ? 1 : 0;
+        const float4* ps = (const float4*)(Pt + sg * BKK + col);
+        const float4* ph = (const float4*)(Pt + (2 + sg) * BKK + col);
+        const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        u32x4* q = (u32x4*)(Xs + cur * 64 * BKK + row * BKK + pc * 8);
+        *q = affine_relu8(*q, sc, sh, true, p.pro_relu != 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * BCO, Xs + cur * 64 * BKK, acc);
   }
   wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
@@ -1141,11 +1208,7 @@ void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
-  size_t lds = (size_t)2 * (BM + BN) * 64 * 2;
-  const size_t cst = (size_t)BM * (BN + 8) * 2;
-  const size_t red = (size_t)(NT / (BN / 8)) * BN * 3 * 4;
-  if (cst > lds) lds = cst;
-  if (red > lds) lds = red;
+  const size_t lds = igemm_glds_pro_offset(BM, BN, NT) + (PRO ? (size_t)2 * a.C * 4 : 0);
   hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI>), dim3(a.nMb * a.nNb), dim3(NT), lds, s,
                      a);
   HIP_CHECK_LAUNCH();
@@ -1229,14 +1292,19 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
-template <int BCO, int BKK, int WM, int WN>
+template <int BCO, int BKK, int WM, int WN, int NST = 2>
 void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   a.nCo = (a.N + BCO - 1) / BCO;
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
-  const size_t lds = (size_t)2 * 64 * (BCO + BKK) * 2;
-  hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
+  const size_t lds = (size_t)NST * 64 * (BCO + BKK) * 2 + (a.pro_sc != nullptr ? 16 * BKK : 0);
+  if (a.pro_sc != nullptr)
+    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, true, NST>), dim3(grid), dim3(64 * WM * WN),
+                       lds, s, a);
+  else
+    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, false, NST>), dim3(grid), dim3(64 * WM * WN),
+                       lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -1255,7 +1323,8 @@ constexpr int IG_GLDS0 = 7;
 constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768}, {64, 64, 768},
                                   {64, 256, 768},  {256, 64, 768},  {128, 128, 512},
                                   {256, 128, 256}, {128, 256, 256}, {256, 256, 256},
-                                  {64, 256, 512},  {128, 128, 256}, {64, 256, 256}};
+                                  {64, 256, 512},  {128, 128, 256}, {64, 256, 256},
+                                  {128, 64, 512},  {128, 128, 256}, {64, 128, 512}};
 constexpr int WG_GLDS0 = 6;
 
 }  // namespace
@@ -1361,8 +1430,8 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.dY2 = f.dY2; a.dp_coef = f.dp_coef; a.dp_seg_rows = f.dp_seg_rows > 0 ? f.dp_seg_rows : a.M;
   a.dp_S = f.dp_S > 0 ? f.dp_S : 1;
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
-  if (wgrad_variant_glds(variant) && (a.pro_sc != nullptr || a.dY2 != nullptr || g.C % 64 != 0)) {
-    fprintf(stderr, "wgrad: LDS-DMA variant %d needs C %% 64 == 0 and no prologue\n", variant);
+  if (wgrad_variant_glds(variant) && !igemm_glds_ok(g, a.pro_sc != nullptr, a.dY2 != nullptr)) {
+    fprintf(stderr, "wgrad: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
     abort();  // the bindings reject this
   }
   switch (variant) {
@@ -1375,6 +1444,9 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 10: launch_wgrad_glds<64, 256, 1, 4>(a, s); break;
     case 11: launch_wgrad_glds<128, 128, 2, 2>(a, s); break;
     case 12: launch_wgrad_glds<64, 256, 1, 4>(a, s); break;
+    case 13: launch_wgrad_glds<128, 64, 2, 2, 3>(a, s); break;
+    case 14: launch_wgrad_glds<128, 128, 2, 2, 3>(a, s); break;
+    case 15: launch_wgrad_glds<64, 128, 2, 2, 3>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;

@@ -139,9 +139,9 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
         ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v,
                   dY2, dcoef, dseg, dS)
 
+    glds_ok = ops.igemm_glds_ok(geom, psc is not None, dpro is not None)
     cands = [v for v in range(ops.wgrad_nvariants())
-             if not (ops.wgrad_variant_glds(v) and (psc is not None or dpro is not None
-                                                    or geom[3] % 64))]
+             if glds_ok or not ops.wgrad_variant_glds(v)]
     v = tuning.pick(key, cands, 1 if N <= 64 else 0,
                     lambda vv: launch(vv, torch.empty_like(out)))
     launch(v, out)
