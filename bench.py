@@ -104,7 +104,13 @@ def run_ours(args, rank, world, dev):
             return next(it)[0]
 
     if args.graph and tr.hip:
-        tr.capture(next_batch())
+        try:
+            tr.capture(next_batch())
+        except Exception as e:  # deterministic across ranks: every rank falls back together
+            print(f"[bench] rank {rank}: hipGraph capture failed ({e!r}); running eager",
+                  file=sys.stderr, flush=True)
+            tr.graph = None
+            args.graph = False
     loss = None
     for _ in range(args.warmup):
         loss = tr.step(next_batch())
@@ -186,14 +192,18 @@ def main(argv=None):
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--gather", action="store_true", help="global negatives (all-gather of z)")
     ap.add_argument("--graph", action="store_true", default=None,
-                    help="capture the step in a hipGraph (default: on for 1 GPU, off for N>1)")
+                    help="capture the step in a hipGraph (default: on)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--bucket-mb", dest="bucket_mb", type=float, default=32.0)
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     args = ap.parse_args(argv)
     rank, world, local, dev = _init()
     if args.graph is None:
-        args.graph = world == 1 and not dist.is_initialized()
+        # the whole step, RCCL collectives included (thread-local capture mode), is one hipGraph
+        # at every N: replays issue no per-kernel host work, so 8 ranks sharing the host CPUs
+        # cannot become launch-bound
+        # (gloo rehearsals on one GPU stay eager: host collectives cannot be captured)
+        args.graph = not dist.is_initialized() or dist.get_backend() == "nccl"
     if args.impl == "ours":
         dt, loss = run_ours(args, rank, world, dev)
     else:

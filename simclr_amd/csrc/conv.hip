@@ -323,7 +323,9 @@ __global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 1 : 2) void igemm_nt(I
   constexpr int BCH = BN * 8 / 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* As = (uint16_t*)smem;          // [2][BM][64]
-  uint16_t* Bs = As + 2 * BM * 64;         // [2][BN][64]
+  // one staging buffer when the whole K fits one tile (the HBM-bound 1x1 convs): the smaller
+  // LDS footprint admits more resident blocks to overlap their load and store phases
+  uint16_t* Bs = As + (p.K > 64 ? 2 : 1) * BM * 64;  // [stages][BN][64]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -495,10 +497,10 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds,
 // Host guarantees: C % 64 == 0 (a 64-wide K slice is one tap), no prologue.
 // byte offset of igemm_glds's prologue table: after the larger of the staging buffers, the
 // epilogue's C image and its statistics scratch
-__host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int NT) {
-  return ((size_t)2 * (BM + BN) * 64 * 2 > (size_t)BM * (BN + 8) * 2
-              ? ((size_t)2 * (BM + BN) * 64 * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
-                     ? (size_t)2 * (BM + BN) * 64 * 2
+__host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int NT, int st) {
+  return ((size_t)st * (BM + BN) * 64 * 2 > (size_t)BM * (BN + 8) * 2
+              ? ((size_t)st * (BM + BN) * 64 * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
+                     ? (size_t)st * (BM + BN) * 64 * 2
                      : (size_t)(NT / (BN / 8)) * BN * 3 * 4)
               : ((size_t)BM * (BN + 8) * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
                      ? (size_t)BM * (BN + 8) * 2
@@ -517,9 +519,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "glds tiling");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* As = (uint16_t*)smem;   // [2][BM][64]
-  uint16_t* Bs = As + 2 * BM * 64;  // [2][BN][64]
+  uint16_t* Bs = As + (p.K > 64 ? 2 : 1) * BM * 64;  // [stages][BN][64] (see igemm_nt)
   // PRO: [sc, sh][C] of the block's segment, behind the staging buffers and the epilogue image
-  float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN));
+  float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN, p.K > 64 ? 2 : 1));
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -1193,7 +1195,7 @@ void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
   const int grid = a.nMb * a.nNb;
-  size_t lds = (size_t)2 * (BM + BN) * 64 * 2;
+  size_t lds = (size_t)(a.K > 64 ? 2 : 1) * (BM + BN) * 64 * 2;
   const size_t cst = (size_t)BM * (BN + 8) * 2;
   const size_t red = (size_t)(256 / (BN / 8)) * BN * 3 * 4;
   if (cst > lds) lds = cst;
@@ -1208,7 +1210,8 @@ void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
-  const size_t lds = igemm_glds_pro_offset(BM, BN, NT) + (PRO ? (size_t)2 * a.C * 4 : 0);
+  const size_t lds =
+      igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? 2 : 1) + (PRO ? (size_t)2 * a.C * 4 : 0);
   hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI>), dim3(a.nMb * a.nNb), dim3(NT), lds, s,
                      a);
   HIP_CHECK_LAUNCH();

@@ -122,6 +122,13 @@ class Trainer:
             for _ in range(warmup):
                 self._step_body(x)
         torch.cuda.current_stream(self.device).wait_stream(s)
+        if self.st.comm:
+            # the RCCL watchdog polls the end events of the eager warm-up collectives; HIP refuses
+            # that query once their stream joins a capture ("event last recorded in a capturing
+            # stream").  Let every eager work complete and be reaped (the watchdog polls every
+            # ~100 ms) before the capture starts.
+            torch.cuda.synchronize(self.device)
+            time.sleep(1.0)
         self._static_x = x.clone()
         g = torch.cuda.CUDAGraph()
         # with collectives in the step, the RCCL watchdog thread polls work events while the
