@@ -121,6 +121,12 @@ class FusedStages:
         self.calls = 0
         # BN backward of a bottleneck's conv3 inside conv3's dgrad/wgrad operand prologues
         self.bnb_prologue = os.environ.get("SIMCLR_BNB_PROLOGUE", "1") != "0"
+        # weight gradients on a second stream (forked after each conv's dY is final, joined at
+        # the end of the backward): they only feed the flat gradient buffer, so they overlap the
+        # dgrad / BatchNorm chain that the next layer's gradient depends on
+        self.wgrad_stream = os.environ.get("SIMCLR_WGRAD_STREAM", "1") != "0"
+        self._side = None
+        self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
         self._wt_cache = {}
@@ -277,8 +283,21 @@ class FusedStages:
         if pro_ss is not None:
             pro = (pro_ss[0], pro_ss[1], M // S, True, S)
         dpro = (bnb[0], bnb[1], M // S, S) if bnb is not None else None
-        _deliver_grad(cs.conv.weight,
-                      lambda out: run_wgrad(ops, dyn, xn, out, g, C, pro=pro, dpro=dpro))
+
+        def run():
+            _deliver_grad(cs.conv.weight,
+                          lambda out: run_wgrad(ops, dyn, xn, out, g, C, pro=pro, dpro=dpro))
+
+        side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
+        if side is None:
+            run()
+            return
+        # operands stay referenced until the join (the caching allocator must not hand their
+        # memory to a main-stream allocation while the side stream still reads them)
+        self._side_keep.extend(t for t in (dyn, xn, pro_ss, *(bnb or ())) if t is not None)
+        side.wait_stream(torch.cuda.current_stream(dyn.device))
+        with torch.cuda.stream(side):
+            run()
 
     def _bnb_ok(self, cs: _ConvSpec, a: torch.Tensor, S: int) -> bool:
         """The BN-backward operand prologue applies to a 1x1 stride-1 conv whose per-segment
@@ -504,12 +523,30 @@ class FusedStages:
         st = pstate.get()
         S = self.S
         self.prepare_backward(ops)
+        main = None
+        if self.wgrad_stream and gout.is_cuda:
+            main = torch.cuda.current_stream(gout.device)
+            if self._side is None or self._side.device != gout.device:
+                self._side = torch.cuda.Stream(device=gout.device)
+            store = self._flat_store()
+            if store is not None:
+                store.producer_streams = [main, self._side]
         g, pre = gout, None
         for idx in range(len(self.blocks) - 1, -1, -1):
             prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else None
             g, pre = self._block_backward(ops, st, S, self.blocks[idx], tapes[idx], g, pre, prev)
+        if main is not None:
+            main.wait_stream(self._side)  # join: every weight gradient is in the flat buffer
+            self._side_keep.clear()
         self._wt_ready = False  # the optimizer step changes the weights
         return g
+
+    def _flat_store(self):
+        for b in self.blocks:
+            slot = getattr(b.convs[0].conv.weight, "_slot", None)
+            if slot is not None:
+                return slot.store
+        return None
 
     def _block_backward(self, ops, st, S, b: _BlockSpec, tp: _BlockTape, g: torch.Tensor,
                         pre, prev):

@@ -91,6 +91,9 @@ class FlatParamStore:
         self.comm = self.world_size > 1 or (world_size is None and group is None and st.comm)
         self._build_buckets(bucket_mb, first_bucket_mb)
         self._comm_stream = None
+        # streams that write gradients (the fused executor adds its weight-gradient stream):
+        # a bucket's all-reduce waits for all of them
+        self.producer_streams: List = []
         self._works: List = []
         self.reset_step()
 
@@ -157,6 +160,9 @@ class FlatParamStore:
                 self._comm_stream = torch.cuda.Stream(device=view.device)
             cur = torch.cuda.current_stream(view.device)
             self._comm_stream.wait_stream(cur)
+            for ps in self.producer_streams:
+                if ps != cur:
+                    self._comm_stream.wait_stream(ps)
             with torch.cuda.stream(self._comm_stream):
                 work = dist.all_reduce(view, group=self.group, async_op=True)
             self._works.append(work)
