@@ -118,8 +118,8 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int bm = igemm_variant_bm((int)variant);
   if (igemm_variant_glds((int)variant))
-    TORCH_CHECK(igemm_glds_ok(g, pro_sc.has_value() && pro_sc->defined(),
-                              pro_d.has_value() && pro_d->defined()),
+    TORCH_CHECK(igemm_variant_ok((int)variant, g, pro_sc.has_value() && pro_sc->defined(),
+                                 pro_d.has_value() && pro_d->defined()),
                 "igemm: LDS-DMA variant needs C % 64 == 0, no BN-backward prologue, and a BN-apply "
                 "prologue only on unpadded 1x1 convolutions");
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
@@ -199,6 +199,12 @@ bool igemm_gldsok(std::vector<int64_t> gv, bool pro, bool bn_bwd_pro) {
 }
 int64_t wgrad_nvariants() { return wgrad_num_variants(); }
 bool wgrad_vglds(int64_t v) { return wgrad_variant_glds((int)v); }
+bool igemm_vok(int64_t v, std::vector<int64_t> gv, bool pro, bool bnb) {
+  return igemm_variant_ok((int)v, geom_from(gv), pro, bnb);
+}
+bool wgrad_vok(int64_t v, std::vector<int64_t> gv, bool pro, bool dpro) {
+  return wgrad_variant_ok((int)v, geom_from(gv), pro, dpro);
+}
 
 int64_t wgrad_nsplit(std::vector<int64_t> gv, int64_t variant) {
   return wgrad_splits(geom_from(gv), (int)variant);
@@ -220,8 +226,8 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
   TORCH_CHECK(creal <= g.C && creal > 0, "wgrad: bad creal");
   TORCH_CHECK(pro_S >= 1 && pro_S <= 2, "wgrad prologue supports at most 2 segments");
   if (wgrad_variant_glds((int)variant))
-    TORCH_CHECK(igemm_glds_ok(g, pro_sc.has_value() && pro_sc->defined(),
-                              dY2.has_value() && dY2->defined()),
+    TORCH_CHECK(wgrad_variant_ok((int)variant, g, pro_sc.has_value() && pro_sc->defined(),
+                                 dY2.has_value() && dY2->defined()),
                 "wgrad: LDS-DMA variant needs C % 64 == 0, no dY prologue, and an X prologue only "
                 "on unpadded 1x1 convolutions");
   ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, pro_S, 0, c10::nullopt,
@@ -663,6 +669,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_glds_ok(int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_gldsok);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
   m.def("wgrad_variant_glds(int v) -> bool", &wgrad_vglds);
+  m.def("igemm_variant_ok(int v, int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_vok);
+  m.def("wgrad_variant_ok(int v, int[] geom, bool pro, bool dy_pro) -> bool", &wgrad_vok);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);

@@ -510,7 +510,9 @@ __host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int N
 // PRO == 1 (1x1 convolutions without padding only, host-checked): the previous BatchNorm's
 // normalise + ReLU is applied to the A tile in LDS after the DMA lands (one read-modify-write
 // pass and one extra barrier per k-tile), so the conv3 forward keeps the DMA pipeline too.
-template <int BM, int BN, int WM, int WN, int PRO, int EPI>
+// NST == 3: three LDS stages; the DMA of tile k+2 is issued while tile k computes and a
+// counted vmcnt keeps tile k+1's DMA in flight across the (raw) barrier.
+template <int BM, int BN, int WM, int WN, int PRO, int EPI, int NST>
 __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -518,10 +520,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // DMA instructions per wave per tile
   static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "glds tiling");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* As = (uint16_t*)smem;   // [2][BM][64]
-  uint16_t* Bs = As + (p.K > 64 ? 2 : 1) * BM * 64;  // [stages][BN][64] (see igemm_nt)
+  const int stages = p.K > 64 ? NST : 1;
+  uint16_t* As = (uint16_t*)smem;          // [stages][BM][64]
+  uint16_t* Bs = As + stages * BM * 64;    // [stages][BN][64] (one stage when K <= 64)
   // PRO: [sc, sh][C] of the block's segment, behind the staging buffers and the epilogue image
-  float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN, p.K > 64 ? 2 : 1));
+  float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN, stages));
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -597,12 +600,20 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       Pt[i] = (i < p.C ? p.pro_sc : p.pro_sh)[pseg * p.C + (i < p.C ? i : i - p.C)];
     __syncthreads();
   }
+  constexpr int PER = AI + BI;  // DMA instructions per wave per k-tile
   issue(0, 0);
+  if (NST == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile kt visible to every wave; every wave is done reading buffer cur^1
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const int cur = NST == 3 ? kt % 3 : kt & 1;
+    if (NST == 3 && kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // tile kt+1 stays in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // raw barrier (__syncthreads() would drain the in-flight DMA): tile kt visible to every
+    // wave, every wave done reading the buffer the next issue overwrites
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
     if (PRO) {
       const int ci0 = kt * 64 - (kt * 64 / p.C) * p.C;
 #pragma unroll
@@ -1204,41 +1215,46 @@ void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
-template <int BM, int BN, int WM, int WN, int PRO, int EPI>
+template <int BM, int BN, int WM, int WN, int PRO, int EPI, int NST>
 void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   IgemmArgs a = a0;
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
   const size_t lds =
-      igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? 2 : 1) + (PRO ? (size_t)2 * a.C * 4 : 0);
-  hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI>), dim3(a.nMb * a.nNb), dim3(NT), lds, s,
-                     a);
+      igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? NST : 1) + (PRO ? (size_t)2 * a.C * 4 : 0);
+  hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI, NST>), dim3(a.nMb * a.nNb), dim3(NT),
+                     lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NST = 2>
 void launch_glds(const IgemmArgs& a, hipStream_t s) {
   if (a.pro_sc != nullptr) {
-    switch (a.epi_mode) {
-      case 1: launch_glds_t<BM, BN, WM, WN, 1, 1>(a, s); break;
-      case 2: launch_glds_t<BM, BN, WM, WN, 1, 2>(a, s); break;
-      case 3: launch_glds_t<BM, BN, WM, WN, 1, 3>(a, s); break;
-      default: launch_glds_t<BM, BN, WM, WN, 1, 0>(a, s); break;
+    if constexpr (NST == 2) {  // the 3-stage tiles leave no LDS for the prologue table
+      switch (a.epi_mode) {
+        case 1: launch_glds_t<BM, BN, WM, WN, 1, 1, NST>(a, s); break;
+        case 2: launch_glds_t<BM, BN, WM, WN, 1, 2, NST>(a, s); break;
+        case 3: launch_glds_t<BM, BN, WM, WN, 1, 3, NST>(a, s); break;
+        default: launch_glds_t<BM, BN, WM, WN, 1, 0, NST>(a, s); break;
+      }
+    } else {
+      fprintf(stderr, "igemm: 3-stage LDS-DMA variant with a prologue\n");
+      abort();  // igemm_variant_ok rejects this
     }
     return;
   }
   switch (a.epi_mode) {
-    case 1: launch_glds_t<BM, BN, WM, WN, 0, 1>(a, s); break;
-    case 2: launch_glds_t<BM, BN, WM, WN, 0, 2>(a, s); break;
-    case 3: launch_glds_t<BM, BN, WM, WN, 0, 3>(a, s); break;
+    case 1: launch_glds_t<BM, BN, WM, WN, 0, 1, NST>(a, s); break;
+    case 2: launch_glds_t<BM, BN, WM, WN, 0, 2, NST>(a, s); break;
+    case 3: launch_glds_t<BM, BN, WM, WN, 0, 3, NST>(a, s); break;
     case 4:
       if (a.stats2 != nullptr)
-        launch_glds_t<BM, BN, WM, WN, 0, 5>(a, s);
+        launch_glds_t<BM, BN, WM, WN, 0, 5, NST>(a, s);
       else
-        launch_glds_t<BM, BN, WM, WN, 0, 4>(a, s);
+        launch_glds_t<BM, BN, WM, WN, 0, 4, NST>(a, s);
       break;
-    default: launch_glds_t<BM, BN, WM, WN, 0, 0>(a, s); break;
+    default: launch_glds_t<BM, BN, WM, WN, 0, 0, NST>(a, s); break;
   }
 }
 
@@ -1317,8 +1333,10 @@ void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
 // variants >= IG_GLDS0 are the LDS-DMA kernel (igemm_glds): no prologue, C % 64 == 0
 constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {64, 64},
                                   {128, 256}, {64, 256},
-                                  {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256}};
-constexpr int IG_GLDS0 = 7;
+                                  {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256},
+                                  {256, 128}, {128, 128}, {128, 256}};
+constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
+constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
 // variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
 // {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
 // that many blocks; every split costs an fp32 N x K slab written here and re-read by the
@@ -1327,7 +1345,8 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {64, 256, 768},  {256, 64, 768},  {128, 128, 512},
                                   {256, 128, 256}, {128, 256, 256}, {256, 256, 256},
                                   {64, 256, 512},  {128, 128, 256}, {64, 256, 256},
-                                  {128, 64, 512},  {128, 128, 256}, {64, 128, 512}};
+                                  {128, 64, 512},  {128, 128, 256}, {64, 128, 512},
+                                  {256, 128, 256}};
 constexpr int WG_GLDS0 = 6;
 
 }  // namespace
@@ -1346,6 +1365,12 @@ bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (g.C % 64 != 0 || bn_bwd_pro) return false;
   // the BN-apply prologue runs on the landed tile: only valid without zero-padding taps
   return !pro || (g.KH == 1 && g.KW == 1 && g.ih0 == 0 && g.iw0 == 0);
+}
+bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
+  if (v < 0 || v >= igemm_num_variants()) return false;
+  if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
+  if (v >= IG_GLDS3 && pro) return false;
+  return igemm_glds_ok(g, pro, bn_bwd_pro);
 }
 int igemm_block_m(int N) { return igemm_variant_bm(igemm_default_variant(N)); }
 
@@ -1373,7 +1398,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
-  if (igemm_variant_glds(variant) && !igemm_glds_ok(g, a.pro_sc != nullptr, a.pro_d != nullptr)) {
+  if (!igemm_variant_ok(variant, g, a.pro_sc != nullptr, a.pro_d != nullptr)) {
     fprintf(stderr, "igemm: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
     abort();  // the bindings reject this; never silently change BM (stats layout)
   }
@@ -1383,6 +1408,9 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 9: launch_glds<256, 64, 4, 1>(a, s); break;
     case 10: launch_glds<128, 128, 2, 2>(a, s); break;
     case 11: launch_glds<128, 256, 2, 4>(a, s); break;
+    case 12: launch_glds<256, 128, 4, 2, 3>(a, s); break;
+    case 13: launch_glds<128, 128, 2, 2, 3>(a, s); break;
+    case 14: launch_glds<128, 256, 2, 4, 3>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
@@ -1396,6 +1424,10 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
 bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < wgrad_num_variants(); }
+bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
+  if (v < 0 || v >= wgrad_num_variants()) return false;
+  return v < WG_GLDS0 || igemm_glds_ok(g, pro, dy_pro);
+}
 
 int wgrad_splits(const ConvGeom& g, int variant) {
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
@@ -1433,7 +1465,7 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.dY2 = f.dY2; a.dp_coef = f.dp_coef; a.dp_seg_rows = f.dp_seg_rows > 0 ? f.dp_seg_rows : a.M;
   a.dp_S = f.dp_S > 0 ? f.dp_S : 1;
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
-  if (wgrad_variant_glds(variant) && !igemm_glds_ok(g, a.pro_sc != nullptr, a.dY2 != nullptr)) {
+  if (!wgrad_variant_ok(variant, g, a.pro_sc != nullptr, a.dY2 != nullptr)) {
     fprintf(stderr, "wgrad: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
     abort();  // the bindings reject this
   }
@@ -1450,6 +1482,7 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 13: launch_wgrad_glds<128, 64, 2, 2, 3>(a, s); break;
     case 14: launch_wgrad_glds<128, 128, 2, 2, 3>(a, s); break;
     case 15: launch_wgrad_glds<64, 128, 2, 2, 3>(a, s); break;
+    case 16: launch_wgrad_glds<256, 128, 2, 2, 3>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;

@@ -52,13 +52,17 @@ int igemm_variant_bn(int v);
 int igemm_default_variant(int N);
 bool igemm_variant_glds(int v);  // LDS-DMA variant (see igemm_glds_ok)
 bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro);
+// can tile variant v run this geometry with these operand prologues (single source of truth for
+// the bindings' checks and the Python autotuner's candidate lists)
+bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro);
 int igemm_block_m(int N);
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
                    uint16_t* out, const float* bias, float* stats, const ConvFusion& f,
                    int variant, hipStream_t s);
 int wgrad_num_variants();
 int wgrad_default_variant(int N);
-bool wgrad_variant_glds(int v);  // LDS-DMA variant: no prologues, needs C % 64 == 0
+bool wgrad_variant_glds(int v);  // LDS-DMA variant (see wgrad_variant_ok)
+bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro);
 int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
                 float* partial, int splits, float* out, int Creal, float beta,

@@ -40,9 +40,8 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
     cands = []
     for v in range(ops.igemm_nvariants()):
         bm = ops.igemm_variant_bm(v)
-        if ops.igemm_variant_glds(v) and not ops.igemm_glds_ok(geom, psc is not None,
-                                                               bnb is not None):
-            continue  # LDS-DMA variants: C % 64 == 0, BN-apply prologue only on unpadded 1x1
+        if not ops.igemm_variant_ok(v, geom, psc is not None, bnb is not None):
+            continue  # e.g. LDS-DMA variants: C % 64 == 0, BN-apply prologue only on 1x1
         if want_stats and M % bm:
             continue
         if psc is not None and pseg % bm:
@@ -139,9 +138,8 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
         ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v,
                   dY2, dcoef, dseg, dS)
 
-    glds_ok = ops.igemm_glds_ok(geom, psc is not None, dpro is not None)
     cands = [v for v in range(ops.wgrad_nvariants())
-             if glds_ok or not ops.wgrad_variant_glds(v)]
+             if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)]
     v = tuning.pick(key, cands, 1 if N <= 64 else 0,
                     lambda vv: launch(vv, torch.empty_like(out)))
     launch(v, out)

@@ -268,7 +268,7 @@ def test_igemm_variants_prologue_epilogue(ops, k, s, p):
     refn = ref.permute(0, 2, 3, 1)
     for v in range(ops.igemm_nvariants()):
         bm = ops.igemm_variant_bm(v)
-        if (M // S) % bm or (ops.igemm_variant_glds(v) and not ops.igemm_glds_ok(g, True, False)):
+        if (M // S) % bm or not ops.igemm_variant_ok(v, g, True, False):
             continue
         out = torch.empty(N, OH, OW, Co, device=DEV, dtype=torch.bfloat16)
         ops.igemm(xn, wo, out, None, None, g, sc, sh, M // S, True, 0, None, None, v)
@@ -284,7 +284,7 @@ def test_igemm_variants_prologue_epilogue(ops, k, s, p):
     yref.backward(gy.float())
     dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
     for v in range(ops.wgrad_nvariants()):
-        if ops.wgrad_variant_glds(v) and not ops.igemm_glds_ok(g, True, False):
+        if not ops.wgrad_variant_ok(v, g, True, False):
             continue
         splits = ops.wgrad_splits(g, v)
         K = k * k * C

@@ -79,7 +79,7 @@ def main():
         g = fwd_geom(N, H, W, Cg, OH, OW, k, k, s, p, Co)
         fw = {}
         for v in range(ops.igemm_nvariants()):
-            if ops.igemm_variant_glds(v) and Cg % 64:
+            if not ops.igemm_variant_ok(v, g, False, False):
                 continue
             fw[v] = timeit(lambda: ops.igemm(x, w, y, None, None, g, None, None, 0, False, 0, None,
                                              None, v))
@@ -91,7 +91,7 @@ def main():
         dyn = torch.randn(N, OH, OW, Co, device=dev).to(torch.bfloat16)
         out = torch.empty(Co, k, k, Cg, device=dev)
         for v in range(ops.wgrad_nvariants()):
-            if ops.wgrad_variant_glds(v) and Cg % 64:
+            if not ops.wgrad_variant_ok(v, g, False, False):
                 continue
             sp = ops.wgrad_splits(g, v)
             part = torch.empty(sp * Co * k * k * Cg, device=dev)

@@ -59,7 +59,7 @@ def main():
                                                  None, None, v)), base)
         res["epi0+st"] = (timeit(lambda: ops.igemm(x, w, y, None, st, g, None, None, 0, False, 0,
                                                     None, None, v)), base)
-        if not glds or ops.igemm_glds_ok(g, True, False):
+        if ops.igemm_variant_ok(v, g, True, False):
             res["pro+st"] = (timeit(lambda: ops.igemm(x, w, y, None, st, g, sc, sh, M // S, True,
                                                        0, None, None, v)), base)
         res["epi4+st"] = (timeit(lambda: ops.igemm(
