@@ -364,19 +364,24 @@ void bn_final(const Tensor& stats, int64_t S, int64_t C, double count, double ep
               optf32(gamma, "gamma"), optf32(beta, "beta"), optf32w(ss, "ss"), cur_stream());
 }
 
-// persistent zeroed ticket array for the last-arriver reductions (per device)
-unsigned* tickets_for(const Tensor& like, int64_t n) {
+// persistent zeroed ticket arrays for the last-arriver reductions, per device and per slot:
+// reductions that may run concurrently (different streams) must use different slots
+constexpr int kTicketSlots = 2;
+constexpr int64_t kTicketStride = 4096;
+unsigned* tickets_for(const Tensor& like, int64_t n, int64_t slot) {
   static std::vector<Tensor> per_dev;
+  TORCH_CHECK(slot >= 0 && slot < kTicketSlots, "ticket slot out of range");
+  TORCH_CHECK(n <= kTicketStride, "too many channel groups for the ticket array");
   const int d = like.get_device();
   if ((int)per_dev.size() <= d) per_dev.resize(d + 1);
-  if (!per_dev[d].defined() || per_dev[d].numel() < n) {
+  if (!per_dev[d].defined()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(cur_stream(), &cs);
     TORCH_CHECK(cs == hipStreamCaptureStatusNone,
                 "bn ticket array must be allocated before graph capture");
-    per_dev[d] = at::zeros({std::max<int64_t>(n, 4096)}, like.options().dtype(at::kInt));
+    per_dev[d] = at::zeros({kTicketSlots * kTicketStride}, like.options().dtype(at::kInt));
   }
-  return reinterpret_cast<unsigned*>(per_dev[d].data_ptr<int>());
+  return reinterpret_cast<unsigned*>(per_dev[d].data_ptr<int>()) + slot * kTicketStride;
 }
 
 void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t C, int64_t mode,
@@ -386,7 +391,7 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
                         const c10::optional<Tensor>& nbt, const c10::optional<Tensor>& gamma,
                         const c10::optional<Tensor>& beta, const c10::optional<Tensor>& ss,
                         const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta,
-                        const c10::optional<Tensor>& coef) {
+                        const c10::optional<Tensor>& coef, int64_t ticket_slot) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "bn_reduce_fused: mode");
   TORCH_CHECK(nblk > 0 && partial.numel() >= S * nblk * 2 * C, "bn_reduce_fused: partial size");
   TORCH_CHECK(C % 4 == 0, "bn_reduce_fused: C must be a multiple of 4 (float4 partial rows)");
@@ -397,7 +402,7 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
   const int G = bn_reduce_groups((int)nblk);
   at::Tensor ws = at::empty({S * G * 2 * C}, partial.options());
   q.ws = ws.data_ptr<float>();
-  q.tickets = tickets_for(partial, (C + 63) / 64);
+  q.tickets = tickets_for(partial, (C + 63) / 64, ticket_slot);
   q.count = (float)count; q.eps = (float)eps; q.momentum = (float)momentum;
   if (mode == 0) {
     TORCH_CHECK(stats.has_value() && stats->numel() >= 2 * S * C, "bn_reduce_fused: stats");
@@ -680,7 +685,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
   m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
-  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None) -> ()", &bn_reduce_fused_op);
+  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0) -> ()", &bn_reduce_fused_op);
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);

@@ -126,6 +126,10 @@ class FusedStages:
         # dgrad / BatchNorm chain that the next layer's gradient depends on
         self.wgrad_stream = os.environ.get("SIMCLR_WGRAD_STREAM", "1") != "0"
         self._side = None
+        # the downsample branch of a stage's first block (forward conv + BN, backward dgrad) on
+        # its own stream, concurrent with the main branch until the block output / conv1 dgrad
+        self.branch_stream = os.environ.get("SIMCLR_BRANCH_STREAM", "1") != "0"
+        self._branch = None
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -192,7 +196,10 @@ class FusedStages:
         igemm_launch(ops, xn, w, a, g, v, stats=stats, pro=pro)
         return a, stats, M // bm // S
 
-    def _bn_fwd(self, ops, bn, partial, nblk_seg: int, rows_seg: int, S: int, st) -> _BNState:
+    def _bn_fwd(self, ops, bn, partial, nblk_seg: int, rows_seg: int, S: int, st,
+                slot: int = 0) -> _BNState:
+        """``slot``: ticket array of the last-arriver reduce (1 on the downsample stream, so a
+        concurrent reduce on the main stream never shares its counters)."""
         C = bn.num_features
         dev = partial.device
         count = float(rows_seg * st.world_size)
@@ -201,10 +208,10 @@ class FusedStages:
         if not st.comm:  # one launch: reduce + finalize (last-arriver)
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
-                                bn.weight.detach(), bn.bias.detach(), ss)
+                                bn.weight.detach(), bn.bias.detach(), ss, None, None, None, slot)
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats)
+            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats, ticket_slot=slot)
             _allreduce(stats, st)
             ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean,
                             bn.running_var, mi, bn.num_batches_tracked, bn.weight.detach(),
@@ -477,10 +484,12 @@ class FusedStages:
         self.calls += 1
         tapes: List[_BlockTape] = []
         x = xn
+        br = self._branch_stream(xn)
         for b in self.blocks:
             tp = _BlockTape(x=x)
             pro_ss = None
             cur = x
+            forked = False
             for ci_, cs in enumerate(b.convs):
                 _ext.TAG = f"{b.name} conv{ci_ + 1} fwd"
                 if pro_ss is not None and cs.k > 1:
@@ -496,18 +505,25 @@ class FusedStages:
                 tp.acts.append(a)
                 tp.bns.append(bs)
                 cur, pro_ss = a, bs.ss
+                if ci_ == 0 and b.down is not None and br is not None:
+                    # fork after BN1 (its statistics all-reduce is issued first, so the branch's
+                    # all-reduce queues behind it on the stats communicator, not in front)
+                    br.wait_stream(torch.cuda.current_stream(x.device))
+                    with torch.cuda.stream(br):
+                        self._down_fwd(ops, b, tp, x, S, st, slot=1)
+                    forked = True
             aL, bsL = tp.acts[-1], tp.bns[-1]
             out = torch.empty_like(aL)
             # the next block's input-gradient epilogue only needs [out > 0]: 1 bit per element
             mask = torch.empty((aL.numel() // 8,), device=aL.device, dtype=torch.uint8)
             _ext.TAG = f"{b.name} ds fwd"
             if b.down is not None:
-                ad, partial, nblk = self._conv_fwd(ops, x, b.down, None, S)
-                rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
-                tp.ad = ad
-                tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st)
+                if forked:
+                    torch.cuda.current_stream(x.device).wait_stream(br)  # join
+                else:
+                    self._down_fwd(ops, b, tp, x, S, st)
                 _ext.TAG = f"{b.name} out fwd"
-                ops.bn_apply_ss(aL, bsL.ss, ad, tp.bnd.ss, out, S, True, mask)
+                ops.bn_apply_ss(aL, bsL.ss, tp.ad, tp.bnd.ss, out, S, True, mask)
             else:
                 _ext.TAG = f"{b.name} out fwd"
                 ops.bn_apply_ss(aL, bsL.ss, x, None, out, S, True, mask)
@@ -517,6 +533,19 @@ class FusedStages:
             x = out
         _ext.TAG = ""
         return x, tapes
+
+    def _branch_stream(self, t: torch.Tensor):
+        if not (getattr(self, "branch_stream", False) and t.is_cuda):
+            return None
+        if self._branch is None or self._branch.device != t.device:
+            self._branch = torch.cuda.Stream(device=t.device)
+        return self._branch
+
+    def _down_fwd(self, ops, b: _BlockSpec, tp: _BlockTape, x, S: int, st, slot: int = 0):
+        ad, partial, nblk = self._conv_fwd(ops, x, b.down, None, S)
+        rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
+        tp.ad = ad
+        tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st, slot=slot)
 
     def backward(self, gout: torch.Tensor, tapes: List[_BlockTape]) -> torch.Tensor:
         ops = _ext.ops()
@@ -601,6 +630,14 @@ class FusedStages:
                     ops.bn_bwd_apply2(g3, aL, coefL, da, tp.ad, coefd, dad, S)
                 else:
                     ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
+        resid_f = None
+        br = self._branch_stream(dad) if dad is not None else None
+        if br is not None:
+            # the downsample dgrad only meets the conv chain at conv1's dgrad epilogue
+            br.wait_stream(torch.cuda.current_stream(dad.device))
+            with torch.cuda.stream(br):
+                _ext.TAG = f"{b.name} ds dgrad"
+                resid_f, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
         # conv chain, last to first: dgrad (+ BN-bwd partials) → start BN all-reduce → wgrad →
         # finish BN → apply
         for i in range(L, 0, -1):
@@ -621,8 +658,12 @@ class FusedStages:
             da = da_next
         cs0 = b.convs[0]
         if b.down is not None:
-            _ext.TAG = f"{b.name} ds dgrad"
-            resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
+            if resid_f is not None:
+                torch.cuda.current_stream(dad.device).wait_stream(br)  # join
+                resid = resid_f
+            else:
+                _ext.TAG = f"{b.name} ds dgrad"
+                resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
         else:
             resid = g3
         _ext.TAG = f"{b.name} conv1 dgrad"
