@@ -660,6 +660,129 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb);
 }
 
+// ------------------------------------------------------------ 3x3 conv, LDS-resident patch
+// 3x3 / stride-1 / pad-1 convolutions (forward, and the stride-1 dgrad, which is the same conv
+// with flipped weights) at 16x16 / 32x32 resolution with 64 or 128 input channels.  The
+// implicit GEMM re-fetches every input pixel once per tap (9x) from L2; with N = 64..128 output
+// channels there are too few MFMAs per fetched byte to hide that (the N = 64 layer1 convs ran at
+// ~0.5 PFLOP/s, L2-bound).  Here a block owns 256 output pixels = 256/OW whole rows of one
+// image, DMAs the (rows + 2) x (OW + 2) x C input patch (halo included, zero padding from
+// out-of-range buffer offsets) into LDS ONCE, and every tap's A fragments are read from that
+// patch at shifted pixel positions; only the weight tile streams per k-step (2 LDS stages).
+// Patch image: [pixel][C] with 16-byte chunk c of pixel q stored at chunk c ^ (q & 7).
+// Host guarantees (igemm_variant_ok): KH = KW = 3, unit strides, ih0 = iw0 = -1, OH = IH,
+// OW = IW in {16, 32}, C in {64, 128}, direct output, no prologue.
+template <int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
+  constexpr int BM = 256;
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int BI = BN / (8 * NW);  // weight DMA instructions per wave per k-step
+  static_assert(BI >= 1 && BI * 8 * NW == BN, "patch tiling");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int C = p.C, OW = p.OW;
+  const int TR = BM / OW;                 // output rows per block
+  const int PW = OW + 2, PP = (TR + 2) * PW;  // patch width / pixels
+  const int ppi = 64 / (C / 8);           // patch pixels per 1 KiB DMA instruction
+  const int ninstr = (PP + ppi - 1) / ppi;
+  uint16_t* Ps = (uint16_t*)smem;         // [PP][C], rounded up to whole DMA instructions
+  uint16_t* Bs = Ps + ninstr * 512;       // [2][BN][64] (the last patch DMA's tail lands before)
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mb = lbid / p.nNb, nb = lbid % p.nNb;
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int OHW = p.OH * OW;
+  const int img = m0 / OHW;
+  const int row0 = (m0 - img * OHW) / OW;
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+
+  // ---- patch DMA: one wave-instruction = 1 KiB = 64 lanes x 16 B (8 or 16 chunks per pixel)
+  const int CPP = C / 8;
+  for (int i = wid; i < ninstr; i += NW) {
+    const int q = i * ppi + lane / CPP;  // patch pixel
+    const int pch = lane % CPP;
+    const int lch = pch ^ (q & 7);
+    const int pr = q / PW, pc = q - (q / PW) * PW;
+    const int ih = row0 - 1 + pr, iw = pc - 1;
+    const bool ok = q < PP && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+    const uint32_t off =
+        ok ? (uint32_t)((((img * p.IH + ih) * p.IW + iw) * C + lch * 8) * 2) : p.a_bytes;
+    dma16(ra, Ps + i * 512, off);  // 512 elements = 1 KiB per instruction
+  }
+  // ---- weight tiles
+  const int lrow = lane >> 3, lbch = (lane & 7) ^ (lane >> 3);
+  uint32_t b_off[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int nrow = n0 + (j * NW + wid) * 8 + lrow;
+    b_off[j] = nrow < p.N ? (uint32_t)(nrow * p.K + lbch * 8) * 2u : p.b_bytes;
+  }
+  auto issue_b = [&](int kt, int buf) {
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      dma16(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)(kt * 64) * 2u);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // per-fragment output pixel (tile-local row r, col c) of this lane's A rows
+  int frow[FM], fcol[FM];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int m = wm * TM + fm * 16 + (lane & 15);
+    frow[fm] = m / OW;
+    fcol[fm] = m - frow[fm] * OW;
+  }
+  const int nk = p.K / 64;
+  issue_b(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch (first step) + weight tile kt
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nk) issue_b(kt + 1, cur ^ 1);
+    const int k0 = kt * 64;
+    const int tap = k0 / C;
+    const int cb = (k0 - tap * C) / 8;  // first logical chunk of this k-step in the pixel
+    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+    const uint16_t* Bb = Bs + cur * BN * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int q = (frow[fm] + kh) * PW + fcol[fm] + kw;
+        const int ch = (cb + ks * 4 + (lane >> 4)) ^ (q & 7);
+        af[fm] = *(const bf16x8*)(Ps + q * C + ch * 8);
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int row = wn * TN + fn * 16 + (lane & 15);
+        const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
+        bfr[fn] = *(const bf16x8*)(Bb + row * 64 + ch * 8);
+      }
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // the epilogue reuses the LDS
+  igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb);
+}
+
 // ------------------------------------------------------------------------------------ wgrad
 // Physical element offset of (row r, element col) in a W-wide swizzled LDS row (see wgrad_tn):
 // 4-element units are XOR-permuted by a row-dependent multiple of 4 units (so 16-byte chunks
@@ -1228,6 +1351,41 @@ void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+size_t igemm_patch_lds(int BN, int NT, int OW, int C) {
+  const int ppi = 64 / (C / 8), pp = (256 / OW + 2) * (OW + 2);
+  const size_t patch = (size_t)((pp + ppi - 1) / ppi) * 1024 + (size_t)2 * BN * 64 * 2;
+  const size_t cst = (size_t)256 * (BN + 8) * 2;
+  const size_t red = (size_t)(NT / (BN / 8)) * BN * 3 * 4;
+  return std::max(patch, std::max(cst, red));
+}
+
+template <int BN, int WM, int WN, int EPI>
+void launch_patch_t(const IgemmArgs& a0, hipStream_t s) {
+  IgemmArgs a = a0;
+  a.nMb = (a.M + 255) / 256;
+  a.nNb = (a.N + BN - 1) / BN;
+  constexpr int NT = 64 * WM * WN;
+  hipLaunchKernelGGL((igemm_patch<BN, WM, WN, EPI>), dim3(a.nMb * a.nNb), dim3(NT),
+                     igemm_patch_lds(BN, NT, a.OW, a.C), s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+template <int BN, int WM, int WN>
+void launch_patch(const IgemmArgs& a, hipStream_t s) {
+  switch (a.epi_mode) {
+    case 1: launch_patch_t<BN, WM, WN, 1>(a, s); break;
+    case 2: launch_patch_t<BN, WM, WN, 2>(a, s); break;
+    case 3: launch_patch_t<BN, WM, WN, 3>(a, s); break;
+    case 4:
+      if (a.stats2 != nullptr)
+        launch_patch_t<BN, WM, WN, 5>(a, s);
+      else
+        launch_patch_t<BN, WM, WN, 4>(a, s);
+      break;
+    default: launch_patch_t<BN, WM, WN, 0>(a, s); break;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int NST = 2>
 void launch_glds(const IgemmArgs& a, hipStream_t s) {
   if (a.pro_sc != nullptr) {
@@ -1334,9 +1492,11 @@ void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
 constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {64, 64},
                                   {128, 256}, {64, 256},
                                   {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256},
-                                  {256, 128}, {128, 128}, {128, 256}};
+                                  {256, 128}, {128, 128}, {128, 256},
+                                  {256, 64}, {256, 128}};
 constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
 constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
+constexpr int IG_PATCH0 = 15;  // 3x3 stride-1 kernel with an LDS-resident input patch
 // variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
 // {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
 // that many blocks; every split costs an fp32 N x K slab written here and re-read by the
@@ -1366,9 +1526,17 @@ bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   // the BN-apply prologue runs on the landed tile: only valid without zero-padding taps
   return !pro || (g.KH == 1 && g.KW == 1 && g.ih0 == 0 && g.iw0 == 0);
 }
+bool igemm_patch_ok(const ConvGeom& g) {
+  const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
+                      g.OWp == g.OW;
+  return g.KH == 3 && g.KW == 3 && g.ish == 1 && g.isw == 1 && g.dh == 1 && g.dw == 1 &&
+         g.ih0 == -1 && g.iw0 == -1 && g.OH == g.IH && g.OW == g.IW &&
+         (g.OW == 16 || g.OW == 32) && (g.C == 64 || g.C == 128) && direct;
+}
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
+  if (v >= IG_PATCH0) return !pro && !bn_bwd_pro && igemm_patch_ok(g);
   if (v >= IG_GLDS3 && pro) return false;
   return igemm_glds_ok(g, pro, bn_bwd_pro);
 }
@@ -1411,6 +1579,8 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 12: launch_glds<256, 128, 4, 2, 3>(a, s); break;
     case 13: launch_glds<128, 128, 2, 2, 3>(a, s); break;
     case 14: launch_glds<128, 256, 2, 4, 3>(a, s); break;
+    case 15: launch_patch<64, 4, 1>(a, s); break;
+    case 16: launch_patch<128, 4, 2>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
