@@ -1210,6 +1210,126 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
   wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
 }
 
+// Weight gradient of a 3x3 / stride-1 / pad-1 convolution (16x16 / 32x32, C in {64, 128}) with
+// the input patch reuse of igemm_patch: a block owns a (64 output channels, 64 input channels)
+// tile of all 9 taps and walks its share of 256-pixel spatial tiles; per tile the dY rows and
+// the halo'd input patch are DMA'd into LDS once (2 stages) and wave t (9 waves) accumulates tap
+// t from them — the implicit GEMM's per-tap re-fetch of the input is gone.  Both operands are
+// read with ds_read_b64_tr_b16 from tr_swz-swizzled images (patch rows = patch pixels, so the
+// B rows of tap (kh, kw) are the pixels (r + kh, c + kw)).  iters_per_split counts 256-row tiles.
+// Host guarantees (wgrad_variant_ok): igemm_patch_ok geometry, N % 64 == 0, no prologues.
+__global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
+  constexpr int B = 64;  // co and ci tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int C = p.C, OW = p.OW;
+  const int lg = OW == 32 ? 5 : 4;
+  const int TR = 256 / OW, PW = OW + 2, PP = (TR + 2) * PW;
+  const int pinstr = (PP + 7) / 8;                 // 8 patch pixels (128 B each) per DMA
+  const int stage = 256 * B + pinstr * 512;        // elements per stage: dY tile + patch
+  uint16_t* S0 = (uint16_t*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;  // wave = tap
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nci = C / B;
+  const int tiles = p.nCo * nci;
+  const int split = lbid / tiles;
+  const int tile = lbid % tiles;
+  const int co0 = (tile / nci) * B, ci0 = (tile % nci) * B;
+  const int ntot = p.M / 256;
+  const int t_beg = split * p.iters_per_split;
+  const int t_end = min(ntot, t_beg + p.iters_per_split);
+  const int OHW = p.OH * OW;
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, (int)p.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
+  const int lr = lane >> 3, lpc = lane & 7;
+
+  auto issue = [&](int t, int buf) {
+    uint16_t* D = S0 + buf * stage;
+    uint16_t* P = D + 256 * B;
+    const int img = (t * 256) / OHW;
+    const int row0 = (t * 256 - img * OHW) >> lg;
+    for (int i = wid; i < 32; i += 9) {  // dY: 8 rows x 128 B per instruction
+      const int r = i * 8 + lr;
+      const int col = co0 + tr_swz<B>(r, lpc * 8);
+      dma16(rd, D + i * 512, (uint32_t)(((size_t)(t * 256 + r) * p.N + col) * 2));
+    }
+    for (int i = wid; i < pinstr; i += 9) {  // patch: 8 pixels x 128 B per instruction
+      const int q = i * 8 + lr;
+      const int ci = ci0 + tr_swz<B>(q, lpc * 8);
+      const int pr = q / PW, pc = q - (q / PW) * PW;
+      const int ih = row0 - 1 + pr, iw = pc - 1;
+      const bool ok = q < PP && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      dma16(rx, P + i * 512,
+            ok ? (uint32_t)((((img * p.IH + ih) * p.IW + iw) * C + ci) * 2) : p.x_bytes);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int kh = wid / 3, kw = wid - (wid / 3) * 3;
+  const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  if (t_beg < t_end) issue(t_beg, 0);
+  for (int t = t_beg; t < t_end; ++t) {
+    const int cur = (t - t_beg) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < t_end) issue(t + 1, cur ^ 1);
+    const uint16_t* D = S0 + cur * stage;
+    const uint16_t* P = D + 256 * B;
+#pragma unroll 2
+    for (int ks = 0; ks < 8; ++ks) {
+      const int r1 = ks * 32 + 8 * g + qq, r2 = r1 + 4;
+      const int q1 = ((r1 >> lg) + kh) * PW + (r1 & (OW - 1)) + kw;
+      const int q2 = ((r2 >> lg) + kh) * PW + (r2 & (OW - 1)) + kw;
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm) {
+        const int col = fm * 16 + 4 * pp;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, D + r1 * B + tr_swz<B>(r1, col)));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, D + r2 * B + tr_swz<B>(r2, col)));
+        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[fm] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        const int col = fn * 16 + 4 * pp;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, P + q1 * B + tr_swz<B>(q1, col)));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, P + q2 * B + tr_swz<B>(q2, col)));
+        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[fn] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+    }
+  }
+  // partial[split][co][tap * C + ci]
+  float* out = p.partial + (size_t)split * p.N * p.K;
+#pragma unroll
+  for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      const int kcol = wid * C + ci0 + fn * 16 + li;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co0 + fm * 16 + g * 4 + i;
+        out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
+      }
+    }
+}
+
 // out[co][tap][ci < Creal] (+)= Σ_s partial[s*stride][co][tap*C + ci]   (slab stride in slabs)
 __global__ void wgrad_reduce(const float* __restrict__ partial, float* __restrict__ out, int splits,
                              int sstride, int N, int K, int C, int Creal, float beta) {
@@ -1506,8 +1626,9 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {256, 128, 256}, {128, 256, 256}, {256, 256, 256},
                                   {64, 256, 512},  {128, 128, 256}, {64, 256, 256},
                                   {128, 64, 512},  {128, 128, 256}, {64, 128, 512},
-                                  {256, 128, 256}};
+                                  {256, 128, 256}, {64, 64, 256}};
 constexpr int WG_GLDS0 = 6;
+constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 
 }  // namespace
 
@@ -1596,6 +1717,7 @@ int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
 bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < wgrad_num_variants(); }
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
+  if (v >= WG_PATCH0) return !pro && !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
   return v < WG_GLDS0 || igemm_glds_ok(g, pro, dy_pro);
 }
 
@@ -1604,11 +1726,13 @@ int wgrad_splits(const ConvGeom& g, int variant) {
   const int bco = WG_VARIANTS[variant][0], bkk = WG_VARIANTS[variant][1];
   const int M = g.Nb * g.OH * g.OW;
   const int K = g.KH * g.KW * g.C;
-  const int tiles = ((g.N + bco - 1) / bco) * ((K + bkk - 1) / bkk);
-  const int iters = (M + 63) / 64;
+  const bool patch = variant >= WG_PATCH0;
+  // the patch kernel's K tile is all 9 taps of 64 input channels; its M unit is 256 rows
+  const int tiles = ((g.N + bco - 1) / bco) * (patch ? g.C / 64 : (K + bkk - 1) / bkk);
+  const int iters = patch ? M / 256 : (M + 63) / 64;
   const int target = WG_VARIANTS[variant][2];
   int splits = (target + tiles - 1) / tiles;
-  int max_splits = iters / 8;
+  int max_splits = patch ? iters : iters / 8;
   if (max_splits < 1) max_splits = 1;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -1626,7 +1750,7 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.ish = g.ish; a.isw = g.isw; a.dh = g.dh; a.dw = g.dw; a.ih0 = g.ih0; a.iw0 = g.iw0;
   a.dy_bytes = (uint32_t)((size_t)a.M * a.N * 2);
   a.x_bytes = (uint32_t)(x_elems * 2);
-  const int iters = (a.M + 63) / 64;
+  const int iters = variant >= WG_PATCH0 ? a.M / 256 : (a.M + 63) / 64;
   a.splits = splits;
   a.iters_per_split = (iters + splits - 1) / splits;
   a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh;
@@ -1653,6 +1777,15 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 14: launch_wgrad_glds<128, 128, 2, 2, 3>(a, s); break;
     case 15: launch_wgrad_glds<64, 128, 2, 2, 3>(a, s); break;
     case 16: launch_wgrad_glds<256, 128, 2, 2, 3>(a, s); break;
+    case 17: {
+      a.nCo = a.N / 64;
+      a.nKk = a.C / 64;
+      const int pp = (256 / a.OW + 2) * (a.OW + 2);
+      const size_t lds = (size_t)2 * (256 * 64 + (pp + 7) / 8 * 512) * 2;
+      hipLaunchKernelGGL(wgrad_patch, dim3(a.nCo * a.nKk * a.splits), dim3(576), lds, s, a);
+      HIP_CHECK_LAUNCH();
+      break;
+    }
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;

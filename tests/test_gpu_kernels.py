@@ -388,7 +388,9 @@ def test_igemm_glds_dgrad_parity_classes(ops):
 
 @pytest.mark.parametrize("k,s,p,C,Co,H", [(1, 1, 0, 64, 256, 16), (3, 1, 1, 64, 64, 16),
                                            (3, 2, 1, 128, 192, 16), (1, 2, 0, 128, 128, 16),
-                                           (3, 1, 1, 256, 512, 4), (3, 1, 1, 64, 64, 5)])
+                                           (3, 1, 1, 256, 512, 4), (3, 1, 1, 64, 64, 5),
+                                           (3, 1, 1, 64, 64, 32), (3, 1, 1, 128, 128, 16),
+                                           (3, 1, 1, 128, 64, 32)])
 def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
     """LDS-DMA weight gradient (wgrad_glds), every tile variant and a few split counts, against
     torch's fp32 conv2d weight gradient (partial M tiles: H=5 gives M % 64 != 0)."""
@@ -405,7 +407,8 @@ def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
     xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
     dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
     K = k * k * C
-    vs = [v for v in range(ops.wgrad_nvariants()) if ops.wgrad_variant_glds(v)]
+    vs = [v for v in range(ops.wgrad_nvariants())
+          if ops.wgrad_variant_glds(v) and ops.wgrad_variant_ok(v, g, False, False)]
     assert vs
     for v in vs:
         base = ops.wgrad_splits(g, v)
