@@ -50,9 +50,10 @@ def _empty_nhwc(n, h, w, c, dev, dtype=torch.bfloat16):
     return torch.empty((n, h, w, c), device=dev, dtype=dtype)
 
 
-def _allreduce(t: torch.Tensor, st) -> None:
+def _allreduce(t: torch.Tensor, st, branch: bool = False) -> None:
     if st.comm:
-        dist.all_reduce(t, group=st.stats_group)
+        g = st.branch_stat_group if branch and st.branch_stat_group is not None else st.stats_group
+        dist.all_reduce(t, group=g)
 
 
 def _deliver_grad(param: torch.Tensor, compute) -> None:
@@ -212,7 +213,7 @@ class FusedStages:
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats, ticket_slot=slot)
-            _allreduce(stats, st)
+            _allreduce(stats, st, branch=slot == 1)
             ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean,
                             bn.running_var, mi, bn.num_batches_tracked, bn.weight.detach(),
                             bn.bias.detach(), ss)
@@ -490,6 +491,13 @@ class FusedStages:
             pro_ss = None
             cur = x
             forked = False
+            if b.down is not None and br is not None:
+                # the downsample conv + BN only meet the main branch at the block output; their
+                # statistics all-reduce uses its own communicator (no ordering with the main's)
+                br.wait_stream(torch.cuda.current_stream(x.device))
+                with torch.cuda.stream(br):
+                    self._down_fwd(ops, b, tp, x, S, st, slot=1)
+                forked = True
             for ci_, cs in enumerate(b.convs):
                 _ext.TAG = f"{b.name} conv{ci_ + 1} fwd"
                 if pro_ss is not None and cs.k > 1:
@@ -505,13 +513,6 @@ class FusedStages:
                 tp.acts.append(a)
                 tp.bns.append(bs)
                 cur, pro_ss = a, bs.ss
-                if ci_ == 0 and b.down is not None and br is not None:
-                    # fork after BN1 (its statistics all-reduce is issued first, so the branch's
-                    # all-reduce queues behind it on the stats communicator, not in front)
-                    br.wait_stream(torch.cuda.current_stream(x.device))
-                    with torch.cuda.stream(br):
-                        self._down_fwd(ops, b, tp, x, S, st, slot=1)
-                    forked = True
             aL, bsL = tp.acts[-1], tp.bns[-1]
             out = torch.empty_like(aL)
             # the next block's input-gradient epilogue only needs [out > 0]: 1 bit per element

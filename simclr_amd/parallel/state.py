@@ -23,6 +23,9 @@ class ParallelState:
     # second communicator for the latency-critical BatchNorm statistics all-reduces, so they
     # never queue behind a multi-MiB gradient-bucket all-reduce on the same RCCL stream
     stat_group: Optional[object] = None
+    # third communicator for the downsample branch's BN statistics (it runs on its own stream,
+    # concurrently with the main branch: sharing a communicator would order their all-reduces)
+    branch_stat_group: Optional[object] = None
     # run every collective even at world_size 1 (a 1-rank RCCL group): exercises the
     # multi-GPU code path (comm streams, async handles, the stats communicator) on one GPU
     force_comm: bool = False
@@ -58,6 +61,7 @@ def make_stat_group(st: "ParallelState") -> None:
     """Create the BN-statistics communicator (collective call: every rank, same order)."""
     if st.comm and st.stat_group is None and dist.is_initialized():
         st.stat_group = dist.new_group(list(range(st.world_size)))
+        st.branch_stat_group = dist.new_group(list(range(st.world_size)))
 
 
 def reset() -> None:
