@@ -54,9 +54,46 @@ def require() -> None:
         raise RuntimeError(f"simclr_amd HIP extension unavailable: {_error}")
 
 
+class _DebugOps:
+    """``SIMCLR_DEBUG=1`` / ``runtime.debug``: every op is followed by a device synchronise, so
+    an asynchronous fault or launch error is reported at the op that caused it, and every
+    floating-point tensor argument (inputs and outputs alike) is checked for NaN/Inf: the first
+    op whose arguments turn non-finite is named in the error."""
+
+    def __init__(self, real):
+        self._real = real
+
+    def __getattr__(self, name):
+        f = getattr(self._real, name)
+        if not callable(f):
+            return f
+
+        def run(*args, **kw):
+            out = f(*args, **kw)
+            if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+                torch.cuda.synchronize()
+                for i, a in enumerate(list(args) + list(kw.values())):
+                    if (isinstance(a, torch.Tensor) and a.is_floating_point() and a.numel()
+                            and not bool(torch.isfinite(a).all())):
+                        raise FloatingPointError(
+                            f"simclr_amd.{name} [{TAG}]: argument {i} {tuple(a.shape)} "
+                            f"{a.dtype} holds NaN/Inf")
+            return out
+
+        return run
+
+
+DEBUG = os.environ.get("SIMCLR_DEBUG", "0") == "1"
+
+
+def set_debug(on: bool) -> None:
+    global DEBUG
+    DEBUG = bool(on)
+
+
 def ops():
     require()
-    return torch.ops.simclr_amd
+    return _DebugOps(torch.ops.simclr_amd) if DEBUG else torch.ops.simclr_amd
 
 
 # Semantic label of the op being issued (set by the fused executor, read by profilers such as

@@ -16,6 +16,13 @@ _CACHE: Dict[Hashable, int] = {}
 ENABLED = os.environ.get("SIMCLR_AUTOTUNE", "1") != "0"
 
 
+def set_enabled(on: bool) -> None:
+    """``runtime.deterministic`` turns tuning off: timing-driven choices differ run to run, and
+    with them the fp32 summation order of a kernel (bitwise reproducibility needs fixed tiles)."""
+    global ENABLED
+    ENABLED = bool(on)
+
+
 def cached(key: Hashable):
     return _CACHE.get(key)
 

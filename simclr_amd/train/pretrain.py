@@ -145,7 +145,18 @@ def pretrain(cfg) -> dict:
     check_pretrain_conf(cfg)
     registry.set_backend(cfg_get(cfg, "runtime.backend", "auto"))
     seed = cfg["parameter"]["seed"]
-    seed_everything(seed, deterministic=bool(cfg_get(cfg, "runtime.deterministic", False)))
+    det = bool(cfg_get(cfg, "runtime.deterministic", False))
+    seed_everything(seed, deterministic=det)
+    if det:
+        from ..ops import tuning
+        tuning.set_enabled(False)
+    if cfg_get(cfg, "runtime.debug", False):
+        from ..ops import _ext
+        _ext.set_debug(True)
+    fault = parse_fault(cfg_get(cfg, "runtime.fault_inject", None)
+                        or os.environ.get("SIMCLR_FAULT_INJECT"))
+    prof_win = parse_window(cfg_get(cfg, "runtime.profile", None))
+    prof = None
     rank = st.rank
     log.info("Using {}".format(st.device))
     ds = load_dataset(cfg["experiment"]["name"], train=True,
@@ -181,11 +192,21 @@ def pretrain(cfg) -> dict:
         t0 = time.time()
         nsteps = 0
         for x, _ in loader:
+            if fault is not None and fault[0] == rank and fault[1] == step_global:
+                log.error("fault injection: rank %d exits with %d at step %d", rank, fault[2],
+                          step_global)
+                logging.shutdown()
+                os._exit(fault[2])
+            if prof_win is not None and step_global == prof_win[0] and prof is None:
+                prof = _start_profiler()
             if use_graph and tr.graph is None:
                 tr.capture(x)
             loss = tr.step(x)
             nsteps += 1
             step_global += 1
+            if prof is not None and step_global >= prof_win[1]:
+                _stop_profiler(prof, rank)
+                prof = None
             if max_steps is not None and step_global >= max_steps:
                 done = True
                 break
@@ -210,6 +231,49 @@ def pretrain(cfg) -> dict:
                                 loader.counter)
         if done:
             break
+    if prof is not None:
+        _stop_profiler(prof, rank)
     summary["wall_seconds"] = time.time() - t_start
     metrics.close()
     return summary
+
+
+def _ints(spec):
+    # "A-B-C" (a YAML string; "A:B" would be read as a base-60 integer) or a [A, B, C] list
+    if isinstance(spec, (list, tuple)):
+        return [int(v) for v in spec]
+    return [int(v) for v in str(spec).replace(",", "-").split("-")]
+
+
+def parse_fault(spec):
+    """``"RANK-STEP[-CODE]"`` → (rank, step, exit code) or None (failure-detection tests)."""
+    if spec is None or spec == "":
+        return None
+    parts = _ints(spec)
+    return parts[0], parts[1], parts[2] if len(parts) > 2 else 13
+
+
+def parse_window(spec):
+    """``"A-B"`` → the global-step window [A, B) traced by torch.profiler, or None."""
+    if spec is None or spec == "":
+        return None
+    a, b = _ints(spec)[:2]
+    return a, b
+
+
+def _start_profiler():
+    acts = [torch.profiler.ProfilerActivity.CPU]
+    if torch.cuda.is_available():
+        acts.append(torch.profiler.ProfilerActivity.CUDA)
+    prof = torch.profiler.profile(activities=acts, record_shapes=False)
+    prof.__enter__()
+    return prof
+
+
+def _stop_profiler(prof, rank: int) -> None:
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    prof.__exit__(None, None, None)
+    path = f"trace-rank{rank}.json"
+    prof.export_chrome_trace(path)
+    log.info("torch.profiler trace written to %s", path)

@@ -64,3 +64,54 @@ def test_supervised_keeps_best_only(tmp_path):
     assert "val acc:" in out
     cks = list(run.glob("epoch=*-cifar10.pt"))
     assert len(cks) == 1
+
+
+@pytest.mark.timeout(600)
+def test_fault_injection_fails_fast(tmp_path):
+    """a rank that dies mid-training (runtime.fault_inject) makes the fail-fast
+    launcher stop its sibling and return the dead rank's exit code, instead of the reference
+    launcher's hang (launch.py:255-259)."""
+    import time
+    t0 = time.time()
+    r = subprocess.run([sys.executable, str(ROOT / "launch.py"), "--nproc_per_node=2",
+                        "--master_port=29617", "--kill_grace=5", "-m", "main", *COMMON,
+                        "parameter.epochs=3", "parameter.warmup_epochs=1",
+                        "runtime.fault_inject=1-2-17", f"hydra.run.dir={tmp_path / 'run'}"],
+                       cwd=str(ROOT), capture_output=True, text=True, timeout=500)
+    assert r.returncode == 17, r.stdout[-2000:] + r.stderr[-2000:]
+    assert time.time() - t0 < 400
+
+
+@pytest.mark.timeout(600)
+def test_profiler_window_writes_trace(tmp_path):
+    run = tmp_path / "run"
+    _run("main.py", COMMON + ["parameter.epochs=1", "runtime.profile=1-3",
+                              "runtime.deterministic=true", f"hydra.run.dir={run}"], tmp_path)
+    trace = json.loads((run / "trace-rank0.json").read_text())
+    assert trace["traceEvents"]
+
+
+def test_debug_ops_wrapper_flags_non_finite():
+    from simclr_amd.ops import _ext
+
+    class Fake:
+        def touch(self, t):
+            return None
+
+    d = _ext._DebugOps(Fake())
+    if torch.cuda.is_available():  # the check runs only where ops run (a GPU)
+        with pytest.raises(FloatingPointError):
+            d.touch(torch.tensor([float("nan")], device="cuda"))
+    d.touch(torch.ones(3))  # finite: passes through
+
+
+def test_deterministic_pins_tile_variants():
+    from simclr_amd.ops import tuning
+    calls = []
+    old = tuning.ENABLED
+    try:
+        tuning.set_enabled(False)
+        v = tuning.pick(("test-key",), [3, 5, 7], 5, lambda v: calls.append(v))
+        assert v == 5 and calls == []  # default variant, no timing trials
+    finally:
+        tuning.set_enabled(old)
