@@ -193,8 +193,9 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
       }
       o[u] = ok[u] ? oo : 0;  // a dead lane reads element 0 and stores nothing
       v[u] = *(const u32x4*)(Cs + row * CST + ch * 8);
-      if (EA) ea[u] = *(const u32x4*)(p.epi_a + o[u]);
-      if (EC) ec[u] = *(const u32x4*)(p.epi_c + o[u]);
+      // streamed operands: read once, nontemporal (no L2 allocation for 0.1-0.5 GB tensors)
+      if (EA) ea[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_a + o[u]));
+      if (EC) ec[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_c + o[u]));
       if (two) ec2[u] = *(const u32x4*)(p.epi_c2 + o[u]);
       if (EB) {
         eb[u] = *(const u32x4*)(p.epi_b + o[u]);
@@ -257,7 +258,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
           }
         }
       }
-      *(u32x4*)(p.out + o[u]) = w;
+      __builtin_nontemporal_store(w, (u32x4*)(p.out + o[u]));
       if (EPI < 3 && p.stats != nullptr) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
