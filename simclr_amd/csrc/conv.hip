@@ -102,12 +102,83 @@ __device__ __forceinline__ u32x4 bnbwd8(u32x4 g, u32x4 x, const float* A, const 
   return w;
 }
 
+// Epilogue row batches: the global operands of UNR output rows (per thread) are loaded together.
+template <int BM, int BN, int NT>
+constexpr int epi_unr() {
+  return (BM / (NT / (BN / 8))) < 4 ? (BM / (NT / (BN / 8))) : 4;
+}
+
+template <int UNR>
+struct EpiBatch {
+  size_t o[UNR];
+  bool ok[UNR];
+  u32x4 ea[UNR], eb[UNR], ec[UNR], ec2[UNR];
+  unsigned bits[UNR];
+};
+
+template <int BM, int BN, int NT, int EPI>
+__device__ __forceinline__ void epi_load_batch(const IgemmArgs& p, int m0, int n0, int it0,
+                                               EpiBatch<epi_unr<BM, BN, NT>()>& b) {
+  constexpr int UNR = epi_unr<BM, BN, NT>();
+  constexpr int CPR = BN / 8, RSTEP = NT / CPR;
+  constexpr bool two = EPI == 5;
+  constexpr bool EA = EPI == 1 || EPI == 2 || EPI == 4 || EPI == 5;
+  constexpr bool EB = EPI == 2 || EPI == 3;
+  constexpr bool EC = EPI == 4 || EPI == 5;
+  const int tid = threadIdx.x;
+  const int ch = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + ch * 8;
+  const int OHW = p.OH * p.OW;
+#pragma unroll
+  for (int u = 0; u < UNR; ++u) {
+    const int row = r0 + (it0 + u) * RSTEP;
+    const int m = m0 + row;
+    b.ok[u] = m < p.M && n < p.N;
+    size_t oo;
+    if (p.direct_out) {
+      oo = (size_t)m * p.ldo + n;
+    } else {
+      const int img = m / OHW;
+      const int rem = m - img * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      oo = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
+    }
+    b.o[u] = b.ok[u] ? oo : 0;  // a dead lane reads element 0 and stores nothing
+    // streamed operands: read once, nontemporal (no L2 allocation for 0.1-0.5 GB tensors)
+    if (EA) b.ea[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_a + b.o[u]));
+    if (EC) b.ec[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_c + b.o[u]));
+    if (two) b.ec2[u] = *(const u32x4*)(p.epi_c2 + b.o[u]);
+    if (EB) {
+      b.eb[u] = *(const u32x4*)(p.epi_b + b.o[u]);
+    } else if (EC) {
+      if (p.epi_mask != nullptr) {
+        b.bits[u] = p.epi_mask[b.o[u] >> 3];
+      } else {
+        const u32x4 y = *(const u32x4*)(p.epi_b + b.o[u]);
+        unsigned bb = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bb |= (lo_bf(y[e]) > 0.f ? 1u : 0u) << (2 * e) | (hi_bf(y[e]) > 0.f ? 2u : 0u) << (2 * e);
+        b.bits[u] = bb;
+      }
+    }
+  }
+}
+
+// Epilogue prefetch: the residual-gradient modes (4/5: three streamed operands per output row,
+// the HBM-heaviest epilogue) load their first row batch before the main loop, so its latency
+// overlaps the operand DMA of the (short-K) GEMM instead of following it.
+template <int EPI>
+constexpr bool epi_prefetch() { return EPI == 4 || EPI == 5; }
+
 // Epilogue shared by the igemm kernels: bias, bf16 round, LDS-staged 16-B row stores, fused
 // elementwise modes 1-5 and the per-block BatchNorm partial statistics (see IgemmArgs).
 template <int BM, int BN, int WM, int WN, int NT, int EPI>
 __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
                                                f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
-                                               char* smem, int m0, int n0, int mb) {
+                                               char* smem, int m0, int n0, int mb,
+                                               const EpiBatch<epi_unr<BM, BN, NT>()>* pre = nullptr) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   static_assert(BN / 8 <= NT && NT % (BN / 8) == 0 && BN <= NT, "epilogue thread mapping");
@@ -166,52 +237,24 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
   // rows in batches of UNR with every global operand load of the batch issued before any is
   // consumed: one row at a time left ~1 load set in flight per wave and ran at ~3.5 TB/s
   constexpr int NIT = BM / RSTEP;
-  constexpr int UNR = NIT < 4 ? NIT : 4;
+  constexpr int UNR = epi_unr<BM, BN, NT>();
   static_assert(NIT % UNR == 0, "epilogue batches");
-  constexpr bool EA = EPI == 1 || EPI == 2 || EPI == 4 || EPI == 5;
-  constexpr bool EB = EPI == 2 || EPI == 3;
-  constexpr bool EC = EPI == 4 || EPI == 5;
   for (int it0 = 0; it0 < NIT; it0 += UNR) {
-    size_t o[UNR];
-    bool ok[UNR];
-    u32x4 v[UNR], ea[UNR], eb[UNR], ec[UNR], ec2[UNR];
-    unsigned bits[UNR];
+    EpiBatch<UNR> B;
+    if (pre != nullptr && it0 == 0)
+      B = *pre;
+    else
+      epi_load_batch<BM, BN, NT, EPI>(p, m0, n0, it0, B);
+    const size_t* o = B.o;
+    const bool* ok = B.ok;
+    const u32x4* ea = B.ea;
+    const u32x4* eb = B.eb;
+    const u32x4* ec = B.ec;
+    const u32x4* ec2 = B.ec2;
+    const unsigned* bits = B.bits;
+    u32x4 v[UNR];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int row = r0 + (it0 + u) * RSTEP;
-      const int m = m0 + row;
-      ok[u] = m < p.M && n < p.N;
-      size_t oo;
-      if (p.direct_out) {
-        oo = (size_t)m * p.ldo + n;
-      } else {
-        const int img = m / OHW;
-        const int rem = m - img * OHW;
-        const int oh = rem / p.OW;
-        const int ow = rem - oh * p.OW;
-        oo = ((size_t)(img * p.OHp + oh * p.osh + p.ooh) * p.OWp + (ow * p.osw + p.oow)) * p.ldo + n;
-      }
-      o[u] = ok[u] ? oo : 0;  // a dead lane reads element 0 and stores nothing
-      v[u] = *(const u32x4*)(Cs + row * CST + ch * 8);
-      // streamed operands: read once, nontemporal (no L2 allocation for 0.1-0.5 GB tensors)
-      if (EA) ea[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_a + o[u]));
-      if (EC) ec[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_c + o[u]));
-      if (two) ec2[u] = *(const u32x4*)(p.epi_c2 + o[u]);
-      if (EB) {
-        eb[u] = *(const u32x4*)(p.epi_b + o[u]);
-      } else if (EC) {
-        if (p.epi_mask != nullptr) {
-          bits[u] = p.epi_mask[o[u] >> 3];
-        } else {
-          const u32x4 y = *(const u32x4*)(p.epi_b + o[u]);
-          unsigned b = 0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            b |= (lo_bf(y[e]) > 0.f ? 1u : 0u) << (2 * e) | (hi_bf(y[e]) > 0.f ? 2u : 0u) << (2 * e);
-          bits[u] = b;
-        }
-      }
-    }
+    for (int u = 0; u < UNR; ++u) v[u] = *(const u32x4*)(Cs + (r0 + (it0 + u) * RSTEP) * CST + ch * 8);
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       if (!ok[u]) continue;
@@ -592,6 +635,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  EpiBatch<epi_unr<BM, BN, NT>()> pre;
+  if (epi_prefetch<EPI>()) epi_load_batch<BM, BN, NT, EPI>(p, m0, n0, 0, pre);
   const int nk = p.K / 64;
   if (PRO) {
     // table staged before any DMA: ordinary global loads consumed in the loop would make hipcc
@@ -658,7 +703,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     }
   }
   __syncthreads();  // the epilogue reuses the staging LDS
-  igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb);
+  igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb,
+                                          epi_prefetch<EPI>() ? &pre : nullptr);
 }
 
 // ------------------------------------------------------------ 3x3 conv, LDS-resident patch
@@ -745,6 +791,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
     frow[fm] = m / OW;
     fcol[fm] = m - frow[fm] * OW;
   }
+  EpiBatch<epi_unr<BM, BN, NT>()> pre;
+  if (epi_prefetch<EPI>()) epi_load_batch<BM, BN, NT, EPI>(p, m0, n0, 0, pre);
   const int nk = p.K / 64;
   issue_b(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
@@ -781,7 +829,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
     }
   }
   __syncthreads();  // the epilogue reuses the LDS
-  igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb);
+  igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb,
+                                          epi_prefetch<EPI>() ? &pre : nullptr);
 }
 
 // ------------------------------------------------------------------------------------ wgrad
