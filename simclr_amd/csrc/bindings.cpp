@@ -105,7 +105,9 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            int64_t stats_base, const c10::optional<Tensor>& epi_c,
            const c10::optional<Tensor>& epi_mask, const c10::optional<Tensor>& epi_c2,
            const c10::optional<Tensor>& epi_mi2, const c10::optional<Tensor>& stats2,
-           const c10::optional<Tensor>& pro_d, const c10::optional<Tensor>& A2) {
+           const c10::optional<Tensor>& pro_d, const c10::optional<Tensor>& A2,
+           const c10::optional<Tensor>& pro_rss, const c10::optional<Tensor>& pro_out,
+           const c10::optional<Tensor>& pro_mask) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -117,11 +119,17 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int bm = igemm_variant_bm((int)variant);
-  if (igemm_variant_glds((int)variant))
+  const bool dual = pro_out.has_value() && pro_out->defined();
+  if (dual) {
+    TORCH_CHECK(igemm_dual_ok((int)variant, g),
+                "igemm: block-output prologue needs a 2-stage LDS-DMA variant (igemm_dual_ok) on "
+                "a 1x1 / stride-1 / unpadded convolution");
+  } else if (igemm_variant_glds((int)variant)) {
     TORCH_CHECK(igemm_variant_ok((int)variant, g, pro_sc.has_value() && pro_sc->defined(),
                                  pro_d.has_value() && pro_d->defined()),
                 "igemm: LDS-DMA variant needs C % 64 == 0, no BN-backward prologue, and a BN-apply "
                 "prologue only on unpadded 1x1 convolutions");
+  }
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
   const bool has_stats = stats.has_value() && stats->defined();
   if (has_stats && stats_seg_blocks == 0)
@@ -185,6 +193,24 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
     f.pro_d = f32(*pro_d, "pro_d");
     f.A2 = bf(*A2, "A2");
   }
+  if (dual) {
+    TORCH_CHECK(f.pro_sc && f.pro_sh && !f.pro_d && epi_mode == 0 && !(bias.has_value() && bias->defined()),
+                "igemm block-output prologue: scale/shift tables, no other fusion");
+    TORCH_CHECK(A2.has_value() && A2->numel() == A.numel(), "igemm block-output prologue: residual");
+    TORCH_CHECK(pro_out->numel() == A.numel(), "igemm block-output prologue: out size");
+    TORCH_CHECK(pro_mask.has_value() && pro_mask->defined() && pro_mask->numel() * 8 >= A.numel(),
+                "igemm block-output prologue: mask size");
+    check_dev(*pro_mask, at::kByte, "pro_mask");
+    f.A2 = bf(*A2, "A2");
+    f.pro_out = bfw(*pro_out, "pro_out");
+    f.pro_mask = pro_mask->data_ptr<uint8_t>();
+    if (pro_rss.has_value() && pro_rss->defined()) {
+      const int64_t nseg = M / pro_seg_rows;
+      TORCH_CHECK(pro_rss->numel() >= 2 * nseg * g.C, "igemm block-output prologue: rss [2][S][C]");
+      f.pro_rsc = f32(*pro_rss, "pro_rss");
+      f.pro_rsh = f.pro_rsc + nseg * g.C;
+    }
+  }
   conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
                 optf32w(stats, "stats"), f, (int)variant, cur_stream());
 }
@@ -202,6 +228,7 @@ bool wgrad_vglds(int64_t v) { return wgrad_variant_glds((int)v); }
 bool igemm_vok(int64_t v, std::vector<int64_t> gv, bool pro, bool bnb) {
   return igemm_variant_ok((int)v, geom_from(gv), pro, bnb);
 }
+bool igemm_dok(int64_t v, std::vector<int64_t> gv) { return igemm_dual_ok((int)v, geom_from(gv)); }
 bool wgrad_vok(int64_t v, std::vector<int64_t> gv, bool pro, bool dpro) {
   return wgrad_variant_ok((int)v, geom_from(gv), pro, dpro);
 }
@@ -665,7 +692,8 @@ void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int6
 }  // namespace
 
 TORCH_LIBRARY(simclr_amd, m) {
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm);
+  m.def("igemm_dual_ok(int v, int[] geom) -> bool", &igemm_dok);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
   m.def("igemm_variant_bm(int v) -> int", &igemm_vbm);

@@ -51,6 +51,13 @@ struct IgemmArgs {
   const float* pro_d;
   const uint16_t* A2;
   int pro_seg_rows, pro_relu;
+  // block-output prologue (igemm_glds PRO == 3): a = relu(A·sc + sh + (A2·rsc + rsh | A2)) —
+  // the previous block's BN3 + downsample BN / identity residual + ReLU — which is also the
+  // block output itself: stored to pro_out with its ReLU bitmask pro_mask (see bn_apply_ss)
+  const float* pro_rsc;
+  const float* pro_rsh;
+  uint16_t* pro_out;
+  uint8_t* pro_mask;
   // epilogue: 0 store, 1 out = acc + epi_a, 2 out = acc + (epi_b > 0 ? epi_a : 0),
   // 3 out = g = (epi_b*sc + sh > 0) ? acc : 0 with BatchNorm-backward partials Σg, Σg·x̂
   //   (x̂ = (epi_b - mean)·invstd) in place of Σy, Σy² (ReLU mask + BN bwd reduce of the
@@ -540,11 +547,13 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds,
 // publishes tile k and runs under tile k's MFMAs; one vmcnt(0) + barrier per k-tile.
 // Host guarantees: C % 64 == 0 (a 64-wide K slice is one tap), no prologue.
 // byte offset of igemm_glds's prologue table: after the larger of the staging buffers, the
-// epilogue's C image and its statistics scratch
-__host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int NT, int st) {
-  return ((size_t)st * (BM + BN) * 64 * 2 > (size_t)BM * (BN + 8) * 2
-              ? ((size_t)st * (BM + BN) * 64 * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
-                     ? (size_t)st * (BM + BN) * 64 * 2
+// epilogue's C image and its statistics scratch (na = 2: the block-output prologue stages the
+// residual tile next to the A tile)
+__host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int NT, int st,
+                                                           int na = 1) {
+  return ((size_t)st * (na * BM + BN) * 64 * 2 > (size_t)BM * (BN + 8) * 2
+              ? ((size_t)st * (na * BM + BN) * 64 * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
+                     ? (size_t)st * (na * BM + BN) * 64 * 2
                      : (size_t)(NT / (BN / 8)) * BN * 3 * 4)
               : ((size_t)BM * (BN + 8) * 2 > (size_t)(NT / (BN / 8)) * BN * 3 * 4
                      ? (size_t)BM * (BN + 8) * 2
@@ -554,6 +563,13 @@ __host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int N
 // PRO == 1 (1x1 convolutions without padding only, host-checked): the previous BatchNorm's
 // normalise + ReLU is applied to the A tile in LDS after the DMA lands (one read-modify-write
 // pass and one extra barrier per k-tile), so the conv3 forward keeps the DMA pipeline too.
+// PRO == 3 (1x1 / stride 1 / unpadded, 2 stages, host-checked): the A operand is the previous
+// block's output, never materialised by a separate pass — the DMA lands both of its inputs
+// (pre-BN conv3 activation and residual) and the prologue pass forms the block output in LDS
+// for the MFMAs and streams it (plus its ReLU bitmask) to HBM from the nb == 0 blocks.  The
+// separate BN-apply kernel and the GEMM's re-read of its output are gone (reference
+// models/resnet.py Bottleneck.forward: out = relu(bn3(conv3) + shortcut), then conv1 of the
+// next block).
 // NST == 3: three LDS stages; the DMA of tile k+2 is issued while tile k computes and a
 // counted vmcnt keeps tile k+1's DMA in flight across the (raw) barrier.
 template <int BM, int BN, int WM, int WN, int PRO, int EPI, int NST>
@@ -565,10 +581,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "glds tiling");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int stages = p.K > 64 ? NST : 1;
+  constexpr int NA = PRO == 3 ? 2 : 1;
   uint16_t* As = (uint16_t*)smem;          // [stages][BM][64]
   uint16_t* Bs = As + stages * BM * 64;    // [stages][BN][64] (one stage when K <= 64)
-  // PRO: [sc, sh][C] of the block's segment, behind the staging buffers and the epilogue image
-  float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN, stages));
+  uint16_t* Rs = Bs + stages * BN * 64;    // PRO 3: [stages][BM][64] residual tile
+  // PRO: [sc, sh (, rsc, rsh)][C] of the block's segment, behind the staging buffers and the
+  // epilogue image
+  float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN, stages, NA));
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -580,6 +599,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(PRO == 3 ? p.A2 : p.A), (short)0, (int)p.a_bytes, 0x00020000);
 
   // lane → (row within its 8-row piece, physical chunk); the logical chunk it fetches is
   // pch ^ (row & 7) = pch ^ lrow (every piece starts at a multiple of 8 rows)
@@ -623,6 +644,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       const uint32_t off =
           ok ? (uint32_t)(((a_pix[j] + ih * p.IW + iw) * p.C + ci) * 2) : OOB_A;
       dma16(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+      if (PRO == 3) dma16(rr, Rs + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j)
@@ -644,15 +666,26 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     const int pseg = m0 / p.pro_seg_rows;  // block-uniform (host guarantees)
     for (int i = tid; i < 2 * p.C; i += NT)
       Pt[i] = (i < p.C ? p.pro_sc : p.pro_sh)[pseg * p.C + (i < p.C ? i : i - p.C)];
+    if (PRO == 3)  // residual scale / shift; identity residual = (1, 0)
+      for (int i = tid; i < 2 * p.C; i += NT) {
+        const int c = i < p.C ? i : i - p.C;
+        Pt[2 * p.C + i] = p.pro_rsc != nullptr
+                              ? (i < p.C ? p.pro_rsc : p.pro_rsh)[pseg * p.C + c]
+                              : (i < p.C ? 1.f : 0.f);
+      }
     __syncthreads();
   }
-  constexpr int PER = AI + BI;  // DMA instructions per wave per k-tile
+  constexpr int PER = NA * AI + BI;  // DMA instructions per wave per k-tile
   issue(0, 0);
   if (NST == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = NST == 3 ? kt % 3 : kt & 1;
     if (NST == 3 && kt + 1 < nk)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // tile kt+1 stays in flight
+    else if (PRO == 3 && nb == 0 && kt > 0)
+      // tile kt's DMA was issued before tile kt-1's block-output stores (2 per chunk, every
+      // wave, M % BM == 0 host-checked): those stay in flight
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * BM * 8 / NT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -660,7 +693,48 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     // wave, every wave done reading the buffer the next issue overwrites
     __builtin_amdgcn_s_barrier();
     if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
-    if (PRO) {
+    if (PRO == 3) {
+      const int ci0 = kt * 64;  // 1x1: K = C
+#pragma unroll
+      for (int i = 0; i < BM * 8 / NT; ++i) {
+        const int c = tid + i * NT;
+        const int row = c >> 3, lc = (c & 7) ^ (row & 7);
+        const int ci = ci0 + lc * 8;
+        u32x4* q = (u32x4*)(As + cur * BM * 64 + c * 8);
+        const u32x4 v = *q, r = *(const u32x4*)(Rs + cur * BM * 64 + c * 8);
+        float tb[4][8];  // sc, sh, rsc, rsh of the chunk's 8 channels (ds_read_b128 x 8)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float4* pt = (const float4*)(Pt + t * p.C + ci);
+          const float4 t0 = pt[0], t1 = pt[1];
+          tb[t][0] = t0.x; tb[t][1] = t0.y; tb[t][2] = t0.z; tb[t][3] = t0.w;
+          tb[t][4] = t1.x; tb[t][5] = t1.y; tb[t][6] = t1.z; tb[t][7] = t1.w;
+        }
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xv = (e & 1) ? hi_bf(v[e >> 1]) : lo_bf(v[e >> 1]);
+          const float rv = (e & 1) ? hi_bf(r[e >> 1]) : lo_bf(r[e >> 1]);
+          o[e] = xv * tb[0][e] + tb[1][e];
+          o[e] += rv * tb[2][e] + tb[3][e];
+          o[e] = fmaxf(o[e], 0.f);
+        }
+        u32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = pack2bf(o[2 * e], o[2 * e + 1]);
+        *q = w;
+        if (nb == 0) {  // block-uniform: every wave issues the same 2 stores per chunk
+          const size_t o8 = (size_t)(m0 + row) * p.C + ci;
+          __builtin_nontemporal_store(w, (u32x4*)(p.pro_out + o8));
+          unsigned bits = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bits |= (o[e] > 0.f ? 1u : 0u) << e;
+          p.pro_mask[o8 / 8] = (uint8_t)bits;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else if (PRO) {
       const int ci0 = kt * 64 - (kt * 64 / p.C) * p.C;
 #pragma unroll
       for (int i = 0; i < BM * 8 / NT; ++i) {
@@ -1514,8 +1588,8 @@ void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
-  const size_t lds =
-      igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? NST : 1) + (PRO ? (size_t)2 * a.C * 4 : 0);
+  const size_t lds = igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? NST : 1, PRO == 3 ? 2 : 1) +
+                     (PRO ? (size_t)(PRO == 3 ? 4 : 2) * a.C * 4 : 0);
   hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI, NST>), dim3(a.nMb * a.nNb), dim3(NT),
                      lds, s, a);
   HIP_CHECK_LAUNCH();
@@ -1558,6 +1632,15 @@ void launch_patch(const IgemmArgs& a, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, int NST = 2>
 void launch_glds(const IgemmArgs& a, hipStream_t s) {
+  if (a.pro_out != nullptr) {  // block-output prologue: 2 stages, plain epilogue (host-checked)
+    if constexpr (NST == 2) {
+      launch_glds_t<BM, BN, WM, WN, 3, 0, NST>(a, s);
+    } else {
+      fprintf(stderr, "igemm: 3-stage LDS-DMA variant with the block-output prologue\n");
+      abort();
+    }
+    return;
+  }
   if (a.pro_sc != nullptr) {
     if constexpr (NST == 2) {  // the 3-stage tiles leave no LDS for the prologue table
       switch (a.epi_mode) {
@@ -1663,10 +1746,12 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
                                   {128, 256}, {64, 256},
                                   {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256},
                                   {256, 128}, {128, 128}, {128, 256},
-                                  {256, 64}, {256, 128}};
+                                  {256, 64}, {256, 128},
+                                  {256, 64}};
 constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
 constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
 constexpr int IG_PATCH0 = 15;  // 3x3 stride-1 kernel with an LDS-resident input patch
+constexpr int IG_GLDS8W = 17;  // 2-stage LDS-DMA, 256 x 64 tile on 8 waves (memory-bound 1x1)
 // variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
 // {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
 // that many blocks; every split costs an fp32 N x K slab written here and re-read by the
@@ -1704,11 +1789,26 @@ bool igemm_patch_ok(const ConvGeom& g) {
          g.ih0 == -1 && g.iw0 == -1 && g.OH == g.IH && g.OW == g.IW &&
          (g.OW == 16 || g.OW == 32) && (g.C == 64 || g.C == 128) && direct;
 }
+// block-output prologue (PRO 3): 2-stage LDS-DMA tiles whose doubled A staging fits the LDS,
+// on 1x1 / stride-1 / unpadded / direct-output convolutions (A row m = output row m)
+bool igemm_dual_ok(int v, const ConvGeom& g) {
+  if (!((v >= IG_GLDS0 && v < IG_GLDS3) || v == IG_GLDS8W) || !igemm_glds_ok(g, true, false))
+    return false;
+  const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
+                      g.OWp == g.OW;
+  if (!(direct && g.ish == 1 && g.isw == 1 && g.OH == g.IH && g.OW == g.IW)) return false;
+  const int BM = IG_VARIANTS[v][0], BN = IG_VARIANTS[v][1];
+  if ((g.Nb * g.OH * g.OW) % BM) return false;  // whole tiles: the kernel counts its stores
+  const int NT = 512;  // upper bound of the tiles' threads (only sizes the stats scratch)
+  const size_t lds = igemm_glds_pro_offset(BM, BN, NT, g.C > 64 ? 2 : 1, 2) + (size_t)16 * g.C;
+  return lds <= 160 * 1024;
+}
+
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
-  if (v >= IG_PATCH0) return !pro && !bn_bwd_pro && igemm_patch_ok(g);
-  if (v >= IG_GLDS3 && pro) return false;
+  if (v >= IG_PATCH0 && v < IG_GLDS8W) return !pro && !bn_bwd_pro && igemm_patch_ok(g);
+  if (v >= IG_GLDS3 && v < IG_PATCH0 && pro) return false;
   return igemm_glds_ok(g, pro, bn_bwd_pro);
 }
 int igemm_block_m(int N) { return igemm_variant_bm(igemm_default_variant(N)); }
@@ -1731,13 +1831,16 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh; a.pro_seg_rows = f.pro_seg_rows > 0 ? f.pro_seg_rows : a.M;
   a.pro_relu = f.pro_relu;
   a.pro_d = f.pro_d; a.A2 = f.A2;
+  a.pro_rsc = f.pro_rsc; a.pro_rsh = f.pro_rsh; a.pro_out = f.pro_out; a.pro_mask = f.pro_mask;
   a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b; a.epi_c = f.epi_c;
   a.epi_mask = f.epi_mask;
   a.epi_c2 = f.epi_c2; a.epi_mi2 = f.epi_mi2; a.stats2 = f.stats2;
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
-  if (!igemm_variant_ok(variant, g, a.pro_sc != nullptr, a.pro_d != nullptr)) {
+  if (a.pro_out != nullptr
+          ? !igemm_dual_ok(variant, g)
+          : !igemm_variant_ok(variant, g, a.pro_sc != nullptr, a.pro_d != nullptr)) {
     fprintf(stderr, "igemm: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
     abort();  // the bindings reject this; never silently change BM (stats layout)
   }
@@ -1752,6 +1855,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 14: launch_glds<128, 256, 2, 4, 3>(a, s); break;
     case 15: launch_patch<64, 4, 1>(a, s); break;
     case 16: launch_patch<128, 4, 2>(a, s); break;
+    case 17: launch_glds<256, 64, 8, 1>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;

@@ -26,6 +26,10 @@ struct ConvFusion {
   int pro_S = 1;
   const float* pro_d = nullptr;   // igemm BN-backward prologue: a = sc·A + sh·A2 + d
   const uint16_t* A2 = nullptr;   //   second A-operand tensor (same geometry as A)
+  const float* pro_rsc = nullptr; // igemm block-output prologue (pro_out != nullptr): a =
+  const float* pro_rsh = nullptr; //   relu(A·sc + sh + A2·rsc + rsh), A2 = residual (rsc null:
+  uint16_t* pro_out = nullptr;    //   identity), a and its ReLU bitmask stored to pro_out /
+  uint8_t* pro_mask = nullptr;    //   pro_mask
   const uint16_t* dY2 = nullptr;  // wgrad dY-operand BN-backward prologue (coef [3][S][N])
   const float* dp_coef = nullptr;
   int dp_seg_rows = 0, dp_S = 1;
@@ -55,6 +59,7 @@ bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro);
 // can tile variant v run this geometry with these operand prologues (single source of truth for
 // the bindings' checks and the Python autotuner's candidate lists)
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro);
+bool igemm_dual_ok(int v, const ConvGeom& g);  // block-output prologue (see igemm_glds)
 int igemm_block_m(int N);
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
                    uint16_t* out, const float* bias, float* stats, const ConvFusion& f,

@@ -131,6 +131,11 @@ class FusedStages:
         # its own stream, concurrent with the main branch until the block output / conv1 dgrad
         self.branch_stream = os.environ.get("SIMCLR_BRANCH_STREAM", "1") != "0"
         self._branch = None
+        # a block's output (BN3 + shortcut + ReLU) formed inside the next block's conv1 prologue
+        # instead of a separate pass that conv1 re-reads.  Off by default: with one 150 KB-LDS
+        # block per CU the fused kernel streams at ~4 TB/s against ~5.5 TB/s for the separate
+        # apply pass, which outweighs the saved re-read except at layer1 (r1 optimisation log)
+        self.block_out_prologue = os.environ.get("SIMCLR_BLOCK_OUT_PROLOGUE", "0") == "1"
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -178,8 +183,13 @@ class FusedStages:
         return True
 
     # ------------------------------------------------------------------ building blocks
-    def _conv_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int):
-        """a = conv(pro(x)) with BN statistics partials in the epilogue."""
+    def _conv_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int,
+                  dual=None):
+        """a = conv(pro(x)) with BN statistics partials in the epilogue.
+
+        ``dual = (aL, ss, res, rss, out, mask)``: the input is the previous block's output,
+        formed in this conv's prologue from that block's conv3 activation ``aL`` and residual
+        ``res`` and written to ``out`` / ``mask`` by the same kernel (``xn`` is ``out``)."""
         Nb, H, W, C = xn.shape
         Co = cs.conv.out_channels
         OH = (H + 2 * cs.pad - cs.k) // cs.stride + 1
@@ -188,14 +198,30 @@ class FusedStages:
         a = _empty_nhwc(Nb, OH, OW, Co, xn.device)
         g = fwd_geom(Nb, H, W, C, OH, OW, cs.k, cs.k, cs.stride, cs.pad, Co)
         M = Nb * OH * OW
-        pro = None
-        if pro_ss is not None:
+        pro, dl, A = None, None, xn
+        if dual is not None:
+            aL, ss, res, rss, out, mask = dual
+            pro = (ss[0], ss[1], M // S, True)
+            dl, A = (res, None if rss is None else rss.view(-1), out, mask), aL
+        elif pro_ss is not None:
             pro = (pro_ss[0], pro_ss[1], M // S, True)
-        v = igemm_choose(ops, xn, w, a, g, want_stats=True, pro=pro, seg_rows=M // S)
+        v = igemm_choose(ops, A, w, a, g, want_stats=True, pro=pro, seg_rows=M // S, dual=dl)
         bm = ops.igemm_variant_bm(v)
         stats = torch.empty(((M // bm) * 2 * Co,), device=xn.device, dtype=torch.float32)
-        igemm_launch(ops, xn, w, a, g, v, stats=stats, pro=pro)
+        igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl)
         return a, stats, M // bm // S
+
+    def _dual_ok(self, ops, xn, cs: _ConvSpec, S: int) -> bool:
+        """Can ``cs`` (a block's conv1) form its input — the previous block's output — in its
+        prologue (1x1 / stride 1 / unpadded, an LDS-DMA tile that fits the doubled staging)?"""
+        if not (getattr(self, "block_out_prologue", False) and xn.is_cuda and cs.k == 1
+                and cs.stride == 1 and cs.pad == 0):
+            return False
+        Nb, H, W, C = xn.shape
+        g = fwd_geom(Nb, H, W, C, H, W, 1, 1, 1, 0, cs.conv.out_channels)
+        M = Nb * H * W
+        return any(ops.igemm_dual_ok(v, g) and (M // S) % ops.igemm_variant_bm(v) == 0
+                   for v in range(ops.igemm_nvariants()))
 
     def _bn_fwd(self, ops, bn, partial, nblk_seg: int, rows_seg: int, S: int, st,
                 slot: int = 0) -> _BNState:
@@ -486,17 +512,29 @@ class FusedStages:
         tapes: List[_BlockTape] = []
         x = xn
         br = self._branch_stream(xn)
+        pend = None  # the previous block's output, not yet formed: (aL, ss, res, rss, out, mask)
         for b in self.blocks:
             tp = _BlockTape(x=x)
             pro_ss = None
             cur = x
+            dual = None
+            if pend is not None:
+                if self._dual_ok(ops, x, b.convs[0], S):
+                    dual = pend  # formed (and written to x) by this block's conv1 prologue
+                else:
+                    self._out_apply(ops, pend, S)
+                pend = None
             forked = False
-            if b.down is not None and br is not None:
+
+            def fork_down():
                 # the downsample conv + BN only meet the main branch at the block output; their
                 # statistics all-reduce uses its own communicator (no ordering with the main's)
                 br.wait_stream(torch.cuda.current_stream(x.device))
                 with torch.cuda.stream(br):
                     self._down_fwd(ops, b, tp, x, S, st, slot=1)
+
+            if b.down is not None and br is not None and dual is None:
+                fork_down()
                 forked = True
             for ci_, cs in enumerate(b.convs):
                 _ext.TAG = f"{b.name} conv{ci_ + 1} fwd"
@@ -507,7 +545,13 @@ class FusedStages:
                     ops.bn_apply_ss(cur, pro_ss, None, None, bmat, S, True)
                     cur, pro_ss = bmat, None
                 tp.ins.append((cur, pro_ss))
-                a, partial, nblk = self._conv_fwd(ops, cur, cs, pro_ss, S)
+                if ci_ == 0 and dual is not None:
+                    a, partial, nblk = self._conv_fwd(ops, cur, cs, None, S, dual=dual)
+                    if b.down is not None and br is not None:
+                        fork_down()  # after the launch that writes its input x
+                        forked = True
+                else:
+                    a, partial, nblk = self._conv_fwd(ops, cur, cs, pro_ss, S)
                 rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
                 bs = self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st)
                 tp.acts.append(a)
@@ -523,17 +567,22 @@ class FusedStages:
                     torch.cuda.current_stream(x.device).wait_stream(br)  # join
                 else:
                     self._down_fwd(ops, b, tp, x, S, st)
-                _ext.TAG = f"{b.name} out fwd"
-                ops.bn_apply_ss(aL, bsL.ss, tp.ad, tp.bnd.ss, out, S, True, mask)
+                pend = (aL, bsL.ss, tp.ad, tp.bnd.ss, out, mask)
             else:
-                _ext.TAG = f"{b.name} out fwd"
-                ops.bn_apply_ss(aL, bsL.ss, x, None, out, S, True, mask)
+                pend = (aL, bsL.ss, x, None, out, mask)
             tp.out = out
             tp.mask = mask
             tapes.append(tp)
             x = out
+        if pend is not None:
+            self._out_apply(ops, pend, S)
         _ext.TAG = ""
         return x, tapes
+
+    def _out_apply(self, ops, pend, S: int) -> None:
+        """Block output = relu(bn3(aL) + shortcut) and its ReLU bitmask, as its own pass."""
+        aL, ss, res, rss, out, mask = pend
+        ops.bn_apply_ss(aL, ss, res, rss, out, S, True, mask)
 
     def _branch_stream(self, t: torch.Tensor):
         if not (getattr(self, "branch_stream", False) and t.is_cuda):

@@ -25,22 +25,28 @@ from . import _ext, tuning
 
 
 def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None,
-                 seg_rows: int = 0, epi_tables=None, bnb=None) -> int:
+                 seg_rows: int = 0, epi_tables=None, bnb=None, dual=None) -> int:
     """Autotuned tile variant for this problem (admissible: BM divides the segment rows /
     M whenever per-segment prologue, statistics or the mode-3 epilogue need block-uniform
-    segments)."""
+    segments).  ``dual = (res, rss, out, mask)``: block-output prologue (see igemm_launch)."""
     M = geom[0] * geom[4] * geom[5]
     N = geom[14]
     psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
     pd, A2 = None, None
     if bnb is not None:  # BN-backward prologue: a = coefA·A + coefB·A2 + coefD
         psc, psh, pd, pseg, A2 = bnb
+    rss, pout, pmask = None, None, None
+    if dual is not None:
+        A2, rss, pout, pmask = dual
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     cands = []
     for v in range(ops.igemm_nvariants()):
         bm = ops.igemm_variant_bm(v)
-        if not ops.igemm_variant_ok(v, geom, psc is not None, bnb is not None):
+        if dual is not None:
+            if not ops.igemm_dual_ok(v, geom):
+                continue
+        elif not ops.igemm_variant_ok(v, geom, psc is not None, bnb is not None):
             continue  # e.g. LDS-DMA variants: C % 64 == 0, BN-apply prologue only on 1x1
         if want_stats and M % bm:
             continue
@@ -56,7 +62,7 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
     if default not in cands:
         default = cands[0]
     key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows,
-           bnb is not None)
+           bnb is not None, dual is not None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
     em = epi[4] if epi is not None and len(epi) > 4 else None
 
@@ -64,28 +70,37 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
         bm = ops.igemm_variant_bm(v)
         st = (torch.empty(((M + bm - 1) // bm) * 2 * N, device=out.device, dtype=torch.float32)
               if want_stats else None)
+        # a block-output trial writes the same values the real launch writes to out / mask
         ops.igemm(A, B, torch.empty_like(out), bias, st, geom, psc, psh, pseg, prelu, emode, ea,
-                  eb, v, ess, emi, seg_rows, 0, 0, ec, em, None, None, None, pd, A2)
+                  eb, v, ess, emi, seg_rows, 0, 0, ec, em, None, None, None, pd, A2, rss, pout,
+                  pmask)
 
     return tuning.pick(key, cands, default, trial)
 
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
                  seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None,
-                 bnb=None) -> None:
+                 bnb=None, dual=None) -> None:
     """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip);
-    ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue."""
+    ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue;
+    ``dual = (res, rss, out, mask)``: block-output prologue — A is a block's pre-BN conv3
+    activation, ``pro`` its BN scale/shift, ``res`` the residual (``rss`` its BN [2][S][C] table
+    or None for identity); the conv consumes relu(bn(A) + res') and also writes it to ``out``
+    with its ReLU bitmask ``mask``."""
     psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
     pd, A2 = None, None
     if bnb is not None:
         psc, psh, pd, pseg, A2 = bnb
+    rss, pout, pmask = None, None, None
+    if dual is not None:
+        A2, rss, pout, pmask = dual
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
     em = epi[4] if epi is not None and len(epi) > 4 else None
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     c2, mi2, st2 = second if second is not None else (None, None, None)
     ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2)
+              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask)
 
 
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):

@@ -178,15 +178,19 @@ def _model(base, stem, device, shadow=torch.bfloat16):
     return m, store
 
 
-@pytest.mark.parametrize("base,stem,batch", [("resnet50", True, 32), ("resnet18", None, 64),
-                                             ("resnet50", True, 64)])
-def test_fused_stages_match_module_path(base, stem, batch):
+@pytest.mark.parametrize("base,stem,batch,block_out", [("resnet50", True, 32, False),
+                                                       ("resnet18", None, 64, False),
+                                                       ("resnet50", True, 64, False),
+                                                       ("resnet50", True, 64, True)])
+def test_fused_stages_match_module_path(base, stem, batch, block_out, monkeypatch):
     """Same weights / input: the executor is at least as close to the fp32 torch reference as
     the per-module bf16 path — loss, every parameter gradient (flat buffer) and every running
     statistic.  (At random init the NT-Xent gradient is a small difference of nearly equal
     embeddings, so bf16 rounding alone moves some gradients by tens of percent: the check is
     relative to the module path's own distance from fp32, not an absolute tolerance.)"""
     from simclr_amd.loss.ntxent import NTXent
+    # block_out: every block output formed in the next conv1's prologue (SIMCLR_BLOCK_OUT_PROLOGUE)
+    monkeypatch.setenv("SIMCLR_BLOCK_OUT_PROLOGUE", "1" if block_out else "0")
     dev = torch.device(DEV, 0)
     torch.manual_seed(5)
     x = _bf(torch.rand(2 * batch, 8, 32, 32, device=dev)).contiguous(

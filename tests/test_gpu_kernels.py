@@ -294,6 +294,55 @@ def test_igemm_variants_prologue_epilogue(ops, k, s, p):
         assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, v
 
 
+@pytest.mark.parametrize("C,Co,H,affine_res", [(256, 64, 16, False), (256, 64, 16, True),
+                                               (512, 128, 8, True), (1024, 256, 4, False),
+                                               (2048, 512, 4, False)])
+def test_igemm_block_output_prologue(ops, C, Co, H, affine_res):
+    """conv1 of the next block forming the block output in its prologue == bn_apply_ss (block
+    output + ReLU mask) followed by the plain conv: out, mask and the BN statistics partials,
+    for every admissible tile (identity and downsample-BN residuals, one or two N tiles)."""
+    from simclr_amd.ops.conv_hip import fwd_geom
+    torch.manual_seed(C + Co)
+    S, N = 2, 16
+    R = N * H * H
+    aL = _bf(torch.randn(R, C, device=DEV))
+    res = _bf(torch.randn(R, C, device=DEV))
+    ss = torch.stack([torch.rand(S, C, device=DEV) + 0.5,
+                      torch.randn(S, C, device=DEV) * 0.3]).contiguous()
+    rss = (torch.stack([torch.rand(S, C, device=DEV) + 0.5, torch.randn(S, C, device=DEV)])
+           .contiguous() if affine_res else None)
+    w = _bf(torch.randn(Co, C, device=DEV) / C ** 0.5)
+    g = fwd_geom(N, H, H, C, H, H, 1, 1, 1, 0, Co)
+    out_ref = torch.empty_like(aL)
+    mask_ref = torch.empty(R * C // 8, device=DEV, dtype=torch.uint8)
+    ops.bn_apply_ss(aL, ss.view(-1), res, None if rss is None else rss.view(-1), out_ref, S, True,
+                    mask_ref)
+    vs = [v for v in range(ops.igemm_nvariants())
+          if ops.igemm_dual_ok(v, g) and (R // S) % ops.igemm_variant_bm(v) == 0]
+    assert vs, "no tile admits the block-output prologue"
+    ref = out_ref.float() @ w.float().t()
+    for v in vs:
+        bm = ops.igemm_variant_bm(v)
+        y0 = torch.empty(R, Co, device=DEV, dtype=torch.bfloat16)
+        st0 = torch.empty((R // bm) * 2 * Co, device=DEV)
+        ops.igemm(out_ref, w, y0, None, st0, g, variant=v)
+        out = torch.full_like(aL, float("nan"))
+        mask = torch.zeros_like(mask_ref)
+        y1 = torch.empty_like(y0)
+        st1 = torch.empty_like(st0)
+        ops.igemm(aL, w, y1, None, st1, g, ss[0].reshape(-1), ss[1].reshape(-1), R // S, True,
+                  variant=v, A2=res, pro_rss=None if rss is None else rss.view(-1), pro_out=out,
+                  pro_mask=mask)
+        torch.cuda.synchronize()
+        d = (out.float() - out_ref.float()).abs()
+        assert d.max().item() <= 1e-2 * out_ref.float().abs().max().item(), v
+        same = (out == out_ref).view(-1, 8).all(1)  # bytes whose 8 outputs agree bit-exactly
+        assert torch.equal(mask[same], mask_ref[same]), v
+        assert same.float().mean().item() > 0.99, v
+        assert _rel(y1, ref) < 1e-2 and _rel(y1, y0) < 1e-2, v
+        assert _rel(st1, st0) < 1e-2, v
+
+
 def _glds_variants(ops):
     return [v for v in range(ops.igemm_nvariants()) if ops.igemm_variant_glds(v)]
 
