@@ -201,6 +201,20 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
     TORCH_CHECK(pro_mask.has_value() && pro_mask->defined() && pro_mask->numel() * 8 >= A.numel(),
                 "igemm block-output prologue: mask size");
     check_dev(*pro_mask, at::kByte, "pro_mask");
+    // the nb == 0 column of blocks writes relu(bn(A) + res) while the other column blocks
+    // still read A / A2: the kernel applies ReLU unconditionally and the output must not alias
+    TORCH_CHECK(pro_relu, "igemm block-output prologue: always applies ReLU (pro_relu required)");
+    auto overlaps = [](const Tensor& a, const Tensor& b) {
+      const char* a0 = static_cast<const char*>(a.data_ptr());
+      const char* b0 = static_cast<const char*>(b.data_ptr());
+      const char* a1 = a0 + a.numel() * a.element_size();
+      const char* b1 = b0 + b.numel() * b.element_size();
+      return a0 < b1 && b0 < a1;
+    };
+    TORCH_CHECK(!overlaps(*pro_out, A) && !overlaps(*pro_out, *A2) && !overlaps(*pro_out, out) &&
+                    !overlaps(*pro_mask, A) && !overlaps(*pro_mask, *A2) && !overlaps(*pro_mask, out),
+                "igemm block-output prologue: out / mask must not alias A, the residual or the "
+                "conv output");
     f.A2 = bf(*A2, "A2");
     f.pro_out = bfw(*pro_out, "pro_out");
     f.pro_mask = pro_mask->data_ptr<uint8_t>();

@@ -78,11 +78,20 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
                       f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *[f"-I{i}" for i in incs], f"-I{py_inc}",
                       "-c", str(b), "-o", str(bo)])
     n = jobs or min(8, os.cpu_count() or 4)
+    conv_rebuilt = any(str(BUILD / "conv.o") in t for t in tasks)
     if tasks:
         with cf.ThreadPoolExecutor(max_workers=n) as ex:
             for out in ex.map(_run, tasks):
                 if verbose and out.strip():
                     print(out)
+    if conv_rebuilt and not debug:
+        # the LDS-DMA pipelines' ordering assumptions, verified on the emitted ISA
+        sys.path.insert(0, str(PKG.parent / "tools"))
+        import isa_check
+        probs = isa_check.check(BUILD / "conv.o")
+        if probs:
+            (BUILD / "conv.o").unlink()
+            raise RuntimeError("ISA check of conv.o failed:\n  " + "\n  ".join(probs[:20]))
     if force or tasks or not OUT.exists() or _stale(OUT, objs):
         tmp = OUT.with_suffix(".so.tmp")
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp),

@@ -535,6 +535,27 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds,
 #endif
 }
 
+// The same DMA, opaque to hipcc's wait-count pass.  That pass cannot tell which LDS bytes an
+// in-flight buffer_load ... lds writes, so it puts s_waitcnt vmcnt(0) in front of the first
+// LDS store (the in-LDS prologues) or ds_read_b64_tr_b16 (the weight gradients) that follows
+// the builtin — draining the NEXT tile's DMA before the current tile computes, i.e. no
+// pipelining at all (tools/isa_check.py finds those drains in the disassembly).  The kernels
+// that use this form order their DMA themselves: a manual vmcnt wait + raw barrier at the top
+// of every k-step covers the landed tile, and the buffer being refilled was released by that
+// barrier.  Compiler-generated vmcnt waits for other loads stay correct (ops hidden from the
+// counter only make its counted waits stricter).  M0 holds the wave-uniform LDS base; these
+// kernels have no other M0 user (checked by tools/isa_check.py), and the s_nop covers the
+// M0-write → LDS-DMA hazard.
+__device__ __forceinline__ void dma16_opaque(__amdgpu_buffer_rsrc_t r, const void* lds,
+                                             uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t base = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)LDS_PTR(const void, lds));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(off), "s"(r), "s"(base) : "memory");
+#endif
+}
+
 // ---------------------------------------------------------------------- igemm, LDS-DMA staged
 // Large-tile implicit GEMM for the compute-bound convolutions (no operand prologue): both
 // operands go HBM/L2 → LDS with buffer_load_dwordx4 … lds (no VGPR round trip, no ds_write
@@ -643,12 +664,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       const bool ok = (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
       const uint32_t off =
           ok ? (uint32_t)(((a_pix[j] + ih * p.IW + iw) * p.C + ci) * 2) : OOB_A;
-      dma16(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
-      if (PRO == 3) dma16(rr, Rs + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+      // the prologues store into the landed tile: the builtin DMA would be drained right
+      // after its issue (see dma16_opaque), so those kernels issue it opaquely
+      if (PRO) {
+        dma16_opaque(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+        if (PRO == 3) dma16_opaque(rr, Rs + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+      } else {
+        dma16(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+      }
     }
 #pragma unroll
-    for (int j = 0; j < BI; ++j)
-      dma16(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)k0 * 2u);
+    for (int j = 0; j < BI; ++j) {
+      if (PRO)
+        dma16_opaque(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)k0 * 2u);
+      else
+        dma16(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)k0 * 2u);
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -1257,7 +1288,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
 #pragma unroll
     for (int j = 0; j < DI; ++j) {
       const bool ok = mb + d_row[j] < mend && d_cok[j];
-      dma16(rd, Ds + buf * 64 * BCO + (j * NW + wid) * RPD * BCO, ok ? d_off[j] : p.dy_bytes);
+      dma16_opaque(rd, Ds + buf * 64 * BCO + (j * NW + wid) * RPD * BCO,
+                   ok ? d_off[j] : p.dy_bytes);
       d_off[j] += dstep;
     }
 #pragma unroll
@@ -1271,7 +1303,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
           (unsigned)iw;
       const uint32_t off = ok ? __umul24(pix, (unsigned)cstride) + (uint32_t)(x_ci[j] * 2)
                               : p.x_bytes;
-      dma16(rx, Xs + buf * 64 * BKK + (j * NW + wid) * RPX * BKK, off);
+      dma16_opaque(rx, Xs + buf * 64 * BKK + (j * NW + wid) * RPX * BKK, off);
       int ow = xow[j] + dow, oh = xoh[j] + doh, n = xn[j] + dn;
       if (ow >= p.OW) { ow -= p.OW; ++oh; }
       if (oh >= p.OH) { oh -= p.OH; ++n; }
@@ -1377,7 +1409,7 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
     for (int i = wid; i < 32; i += 9) {  // dY: 8 rows x 128 B per instruction
       const int r = i * 8 + lr;
       const int col = co0 + tr_swz<B>(r, lpc * 8);
-      dma16(rd, D + i * 512, (uint32_t)(((size_t)(t * 256 + r) * p.N + col) * 2));
+      dma16_opaque(rd, D + i * 512, (uint32_t)(((size_t)(t * 256 + r) * p.N + col) * 2));
     }
     for (int i = wid; i < pinstr; i += 9) {  // patch: 8 pixels x 128 B per instruction
       const int q = i * 8 + lr;
@@ -1385,7 +1417,7 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
       const int pr = q / PW, pc = q - (q / PW) * PW;
       const int ih = row0 - 1 + pr, iw = pc - 1;
       const bool ok = q < PP && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-      dma16(rx, P + i * 512,
+      dma16_opaque(rx, P + i * 512,
             ok ? (uint32_t)((((img * p.IH + ih) * p.IW + iw) * C + ci) * 2) : p.x_bytes);
     }
   };

@@ -70,10 +70,13 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
         bm = ops.igemm_variant_bm(v)
         st = (torch.empty(((M + bm - 1) // bm) * 2 * N, device=out.device, dtype=torch.float32)
               if want_stats else None)
-        # a block-output trial writes the same values the real launch writes to out / mask
+        # every output of a trial is scratch (tuning.py: trials touch no live tensor), the
+        # block-output prologue's out / mask included
+        tout = torch.empty_like(pout) if pout is not None else None
+        tmask = torch.empty_like(pmask) if pmask is not None else None
         ops.igemm(A, B, torch.empty_like(out), bias, st, geom, psc, psh, pseg, prelu, emode, ea,
-                  eb, v, ess, emi, seg_rows, 0, 0, ec, em, None, None, None, pd, A2, rss, pout,
-                  pmask)
+                  eb, v, ess, emi, seg_rows, 0, 0, ec, em, None, None, None, pd, A2, rss, tout,
+                  tmask)
 
     return tuning.pick(key, cands, default, trial)
 
