@@ -120,6 +120,9 @@ class FusedStages:
         self.resnet = resnet
         self.S = segments
         self.calls = 0
+        # launch accounting (tests): block outputs formed in a conv1 prologue / as their own pass
+        self.dual_launches = 0
+        self.out_apply_calls = 0
         # BN backward of a bottleneck's conv3 inside conv3's dgrad/wgrad operand prologues
         self.bnb_prologue = os.environ.get("SIMCLR_BNB_PROLOGUE", "1") != "0"
         # weight gradients on a second stream (forked after each conv's dY is final, joined at
@@ -132,10 +135,13 @@ class FusedStages:
         self.branch_stream = os.environ.get("SIMCLR_BRANCH_STREAM", "1") != "0"
         self._branch = None
         # a block's output (BN3 + shortcut + ReLU) formed inside the next block's conv1 prologue
-        # instead of a separate pass that conv1 re-reads.  Off by default: with one 150 KB-LDS
-        # block per CU the fused kernel streams at ~4 TB/s against ~5.5 TB/s for the separate
-        # apply pass, which outweighs the saved re-read except at layer1 (r1 optimisation log)
-        self.block_out_prologue = os.environ.get("SIMCLR_BLOCK_OUT_PROLOGUE", "0") == "1"
+        # instead of a separate pass that conv1 re-reads.  SIMCLR_BLOCK_OUT_PROLOGUE: 0 = off,
+        # N >= 1 = on for blocks whose maps are at least N x N (1 = every block, the default:
+        # since the prologue kernels keep their DMA pipelined it wins at every stage —
+        # 24.06 -> 23.80 ms/step A/B, r2 optimisation log)
+        v = os.environ.get("SIMCLR_BLOCK_OUT_PROLOGUE", "1")
+        self.block_out_min_hw = int(v) if v.isdigit() else 1
+        self.block_out_prologue = self.block_out_min_hw > 0
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -218,6 +224,8 @@ class FusedStages:
                 and cs.stride == 1 and cs.pad == 0):
             return False
         Nb, H, W, C = xn.shape
+        if H < getattr(self, "block_out_min_hw", 1):
+            return False
         g = fwd_geom(Nb, H, W, C, H, W, 1, 1, 1, 0, cs.conv.out_channels)
         M = Nb * H * W
         return any(ops.igemm_dual_ok(v, g) and (M // S) % ops.igemm_variant_bm(v) == 0
@@ -547,6 +555,7 @@ class FusedStages:
                 tp.ins.append((cur, pro_ss))
                 if ci_ == 0 and dual is not None:
                     a, partial, nblk = self._conv_fwd(ops, cur, cs, None, S, dual=dual)
+                    self.dual_launches += 1
                     if b.down is not None and br is not None:
                         fork_down()  # after the launch that writes its input x
                         forked = True
@@ -582,6 +591,7 @@ class FusedStages:
     def _out_apply(self, ops, pend, S: int) -> None:
         """Block output = relu(bn3(aL) + shortcut) and its ReLU bitmask, as its own pass."""
         aL, ss, res, rss, out, mask = pend
+        self.out_apply_calls += 1
         ops.bn_apply_ss(aL, ss, res, rss, out, S, True, mask)
 
     def _branch_stream(self, t: torch.Tensor):

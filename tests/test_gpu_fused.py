@@ -214,6 +214,12 @@ def test_fused_stages_match_module_path(base, stem, batch, block_out, monkeypatc
         if mode == "fused":
             ex = m2.f.__dict__.get("_fused_cache", {}).get(2)
             assert ex is not None and ex.calls == 1, "fused executor did not run"
+            nblk = len(ex.blocks)
+            if block_out:  # every 1x1 conv1 after the first block formed its input itself
+                assert (ex.dual_launches, ex.out_apply_calls) == (nblk - 1, 1), \
+                    (ex.dual_launches, ex.out_apply_calls)
+            else:
+                assert (ex.dual_launches, ex.out_apply_calls) == (0, nblk)
         res[mode] = (float(loss.detach()), store2.grad.clone(),
                      [(n, b.float().clone()) for n, b in m2.named_buffers() if "running" in n])
     lm, gm, bm = res["module"]
