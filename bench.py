@@ -80,6 +80,9 @@ def run_ours(args, rank, world, dev):
         force_comm=dist.is_initialized())
     st.device = dev
     pstate.make_stat_group(st)
+    if st.comm and dev.type == "cuda":
+        from simclr_amd.comm import setup_stats_exchange
+        setup_stats_exchange(st, dev)  # IPC BatchNorm statistics (self-tested, else RCCL)
     ov = [f"experiment.base_cnn={args.model}", f"experiment.batches={args.batch}",
           f"model.cifar_stem={'true' if args.cifar_stem else 'null'}",
           "data.synthetic=true", f"runtime.precision={args.precision}",
@@ -93,6 +96,7 @@ def run_ours(args, rank, world, dev):
                                strength=cfg["experiment"]["strength"], seed=7, views=2)
     tr = Trainer(cfg, st, 50000)
     it = iter(loader)
+    args.bn_comm = ("ipc" if st.ipc is not None else "rccl") if st.comm else "none"
 
     def next_batch():
         nonlocal it
@@ -204,6 +208,7 @@ def main(argv=None):
         # cannot become launch-bound
         # (gloo rehearsals on one GPU stay eager: host collectives cannot be captured)
         args.graph = not dist.is_initialized() or dist.get_backend() == "nccl"
+    args.bn_comm = "none"
     if args.impl == "ours":
         dt, loss = run_ours(args, rank, world, dev)
     else:
@@ -253,6 +258,7 @@ def main(argv=None):
             "optimizer": "LARS(trust=1e-3)+SGD(m=0.9), warmup+cosine",
             "impl": args.impl,
             "hip_graph": bool(args.graph and args.impl == "ours"),
+            "bn_stats_comm": args.bn_comm,
             "host_issue_ms_per_step": (round(args.host_issue_ms, 3)
                                        if hasattr(args, "host_issue_ms") else None),
             "final_loss": loss,

@@ -1,0 +1,3 @@
+"""Communication layer beyond RCCL: one-shot IPC exchange of BatchNorm statistics over xGMI
+(``ipc.IpcStatsExchange``).  Bulk gradient all-reduce stays on RCCL (parallel/flat.py)."""
+from .ipc import IpcStatsExchange, setup_stats_exchange  # noqa: F401

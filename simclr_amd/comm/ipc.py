@@ -1,0 +1,189 @@
+"""One-shot cross-rank exchange of BatchNorm statistics through IPC-mapped device memory.
+
+Reference behaviour replaced: SyncBatchNorm issues an ``all_gather`` of [mean‖invstd‖count]
+per BN layer per forward and an ``all_reduce`` of [Σdy‖Σdy·x̂] per BN layer in backward
+(/root/reference/main.py:176 → torch/nn/modules/_functions.py:74,159): ~2x53 latency-bound
+collectives per ResNet-50 step, each a separate NCCL launch on the critical path.
+The RCCL path of this framework already halves that (one all-reduce of both views' [Σ, Σ²]
+per layer, csrc/bn.hip + models/fused.py); this module removes the collective launches
+altogether on a single node: the fused BN reduce kernel that finalizes a layer's statistics
+pushes its local sums straight into every peer's arena over xGMI and sums the W slots of its
+own arena in rank order (csrc/bn.hip ``bn_ipc_exchange``) — one kernel per BatchNorm, no
+RCCL, no host involvement, capturable in the step's hipGraph, bitwise-identical statistics on
+every rank.
+
+Arena layout: int64 words; every BatchNorm site (a (module, direction) pair, allocated in
+first-call order, which is identical on all ranks of an SPMD step) owns
+``2 parities x world x [2][S][C]`` words at the same offset in every rank's arena, and
+``ceil(C/64)`` epoch counters in a local int32 buffer.
+
+``setup_stats_exchange`` builds the exchange only when every rank can (same node, GPU,
+world <= 16) and keeps it only if a self-test — two exchanges against host-computed sums —
+passes on every rank; otherwise the step falls back to the RCCL statistics all-reduce.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+
+DEFAULT_WORDS = 1 << 23  # 64 MiB arena: ResNet-50 fwd + bwd sites at W = 8 need ~30 MiB
+MAX_WORLD = 16
+
+
+def region_words(world: int, S: int, C: int) -> int:
+    """Words of one site's region (mirrors kernels.h bn_ipc_region_words)."""
+    return 2 * world * 2 * S * C
+
+
+class SiteTable:
+    """Deterministic sub-allocation of arena regions and epoch counters (host-only logic)."""
+
+    def __init__(self, world: int, words: int, epochs: int):
+        self.world = world
+        self.words = words
+        self.epochs = epochs
+        self.sites: Dict[object, Tuple[int, int, int, int]] = {}
+        self.next_word = 0
+        self.next_epoch = 0
+
+    def get(self, key, S: int, C: int) -> Tuple[int, int, int]:
+        """(word offset, epoch offset, epoch count) of ``key``'s region (allocated on first use;
+        a key seen again with another shape is an error: the peers hold the old layout)."""
+        if key in self.sites:
+            off, eo, ne, shape = self.sites[key]
+            if shape != S * 100000 + C:
+                raise ValueError(f"IPC site {key!r} reused with another shape (S={S}, C={C})")
+            return off, eo, ne
+        n = region_words(self.world, S, C)
+        ne = (C + 63) // 64
+        if self.next_word + n > self.words or self.next_epoch + ne > self.epochs:
+            raise RuntimeError("IPC statistics arena exhausted "
+                               f"({self.next_word + n} > {self.words} words)")
+        rec = (self.next_word, self.next_epoch, ne, S * 100000 + C)
+        self.sites[key] = rec
+        self.next_word += n
+        self.next_epoch += ne
+        return rec[:3]
+
+
+class IpcStatsExchange:
+    def __init__(self, rank: int, world: int, device: torch.device, group=None,
+                 words: int = DEFAULT_WORDS, epochs: int = 1 << 16):
+        if world > MAX_WORLD:
+            raise ValueError(f"IPC exchange supports at most {MAX_WORLD} ranks")
+        ops = _ext.ops()
+        self.rank, self.world, self.device = rank, world, device
+        self.arena = ops.ipc_arena_alloc(words, device.index)
+        handle = ops.ipc_handle(self.arena)
+        handles: List[Optional[bytes]] = [None] * world
+        dist.all_gather_object(handles, bytes(handle.numpy().tobytes()), group=group)
+        self._opened: List[int] = []
+        ptrs = []
+        for r, hb in enumerate(handles):
+            if r == rank:
+                ptrs.append(self.arena.data_ptr())
+                continue
+            p = ops.ipc_open(torch.frombuffer(bytearray(hb), dtype=torch.uint8), device.index)
+            self._opened.append(p)
+            ptrs.append(p)
+        self.peers = torch.tensor(ptrs, dtype=torch.int64, device=device)
+        self.epoch = torch.zeros(epochs, dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.table = SiteTable(world, words, epochs)
+
+    def kwargs(self, key, S: int, C: int) -> dict:
+        """Extra arguments of ``bn_reduce_fused`` (modes 1 / 2) for site ``key``."""
+        off, eo, ne = self.table.get(key, S, C)
+        return dict(ipc_peers=self.peers, ipc_arena=self.arena, ipc_site=off,
+                    ipc_epoch=self.epoch[eo:eo + ne], ipc_err=self.err, world=self.world,
+                    rank=self.rank)
+
+    def failed(self) -> bool:
+        """A spin timed out (a peer never delivered): the statistics of that step are wrong."""
+        return bool(self.err.item())
+
+    def close(self) -> None:
+        ops = _ext.ops()
+        for p in self._opened:
+            try:
+                ops.ipc_close(p)
+            except Exception:
+                pass
+        self._opened = []
+
+    # ------------------------------------------------------------------ self-test
+    def selftest(self, rounds: int = 3) -> bool:
+        """Exchange rank-dependent sums through a dedicated site ``rounds`` times (both arena
+        parities) and compare the finalized mean / invstd with the host-computed values."""
+        ops = _ext.ops()
+        S, C, nblk = 2, 192, 3
+        dev = self.device
+        ok = True
+        for it in range(rounds):
+            c = torch.arange(C, dtype=torch.float64)
+            part = torch.zeros(S, nblk, 2, C, dtype=torch.float64)
+            tot1 = torch.zeros(S, C, dtype=torch.float64)
+            tot2 = torch.zeros(S, C, dtype=torch.float64)
+            for r in range(self.world):
+                for s in range(S):
+                    for b in range(nblk):
+                        v1 = (r + 1) * 0.25 + s + 0.01 * c + b + it
+                        v2 = v1 * v1 + 1.0 + 0.1 * r
+                        if r == self.rank:
+                            part[s, b, 0] = v1
+                            part[s, b, 1] = v2
+                        tot1[s] += v1
+                        tot2[s] += v2
+            count = float(nblk * self.world)
+            mean = tot1 / count
+            var = (tot2 / count - mean * mean).clamp_min(0)
+            inv = 1.0 / torch.sqrt(var + 1e-5)
+            mi = torch.empty(2 * S * C, dtype=torch.float32, device=dev)
+            ops.bn_reduce_fused(part.float().reshape(-1).to(dev), nblk, S, C, 1, None, count,
+                                1e-5, 0.1, None, None, mi, None, None, None, None, None, None,
+                                None, 0, **self.kwargs("__selftest__", S, C))
+            got = mi.view(2, S, C).double().cpu()
+            ok = ok and torch.allclose(got[0], mean, rtol=1e-4, atol=1e-4) and \
+                torch.allclose(got[1], inv, rtol=1e-3, atol=1e-3)
+        torch.cuda.synchronize(dev)
+        return ok and not self.failed()
+
+
+def setup_stats_exchange(st, device: torch.device, mode: Optional[str] = None):
+    """Attach an IPC statistics exchange to the parallel state ``st`` when it applies.
+
+    ``mode`` (or ``SIMCLR_BN_COMM``): ``rccl`` never, ``ipc`` always (raise if impossible),
+    ``auto`` (default) at world > 1 on GPUs when the self-test passes on every rank."""
+    mode = (mode or os.environ.get("SIMCLR_BN_COMM", "auto")).lower()
+    st.ipc = None
+    if mode == "rccl" or not st.comm or st.world_size < 2 or device.type != "cuda":
+        if mode == "ipc" and st.world_size > 1 and device.type != "cuda":
+            raise RuntimeError("SIMCLR_BN_COMM=ipc needs GPUs")
+        return None
+    ex, ok = None, 0
+    try:
+        if st.world_size <= MAX_WORLD and _ext.available():
+            ex = IpcStatsExchange(st.rank, st.world_size, device, group=st.group)
+            ok = int(ex.selftest())
+    except Exception as e:  # every rank takes the same decision below
+        print(f"[ipc] rank {st.rank}: exchange setup failed: {e!r}", file=sys.stderr, flush=True)
+        ok = 0
+    flag = torch.tensor([ok], dtype=torch.int32,
+                        device=device if dist.get_backend(st.group) == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=st.group)
+    if int(flag.item()) != 1:
+        if ex is not None:
+            ex.close()
+        if mode == "ipc":
+            raise RuntimeError("IPC statistics exchange failed its self-test")
+        print(f"[ipc] rank {st.rank}: IPC statistics exchange unavailable, using RCCL",
+              file=sys.stderr, flush=True)
+        return None
+    st.ipc = ex
+    return ex

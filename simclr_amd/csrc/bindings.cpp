@@ -432,7 +432,11 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
                         const c10::optional<Tensor>& nbt, const c10::optional<Tensor>& gamma,
                         const c10::optional<Tensor>& beta, const c10::optional<Tensor>& ss,
                         const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta,
-                        const c10::optional<Tensor>& coef, int64_t ticket_slot) {
+                        const c10::optional<Tensor>& coef, int64_t ticket_slot,
+                        const c10::optional<Tensor>& ipc_peers,
+                        const c10::optional<Tensor>& ipc_arena, int64_t ipc_site,
+                        const c10::optional<Tensor>& ipc_epoch,
+                        const c10::optional<Tensor>& ipc_err, int64_t world, int64_t rank) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "bn_reduce_fused: mode");
   TORCH_CHECK(nblk > 0 && partial.numel() >= S * nblk * 2 * C, "bn_reduce_fused: partial size");
   TORCH_CHECK(C % 4 == 0, "bn_reduce_fused: C must be a multiple of 4 (float4 partial rows)");
@@ -474,6 +478,30 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
   if (q.beta) TORCH_CHECK(beta->numel() == C, "bn_reduce_fused: beta size");
   if (q.dgamma) TORCH_CHECK(dgamma->numel() == C, "bn_reduce_fused: dgamma size");
   if (q.dbeta) TORCH_CHECK(dbeta->numel() == C, "bn_reduce_fused: dbeta size");
+  if (world > 1) {
+    // IPC statistics exchange (bn.hip bn_ipc_exchange): every rank's arena must hold this
+    // site's region, the peer table one base per rank, the epochs one counter per channel group
+    TORCH_CHECK(mode == 1 || mode == 2, "bn_reduce_fused: the IPC exchange finalizes (mode 1/2)");
+    TORCH_CHECK(world <= 16 && rank >= 0 && rank < world, "bn_reduce_fused: world / rank");
+    TORCH_CHECK(ipc_peers.has_value() && ipc_arena.has_value() && ipc_epoch.has_value() &&
+                    ipc_err.has_value(), "bn_reduce_fused: IPC exchange needs peers, arena, epoch, err");
+    check_dev(*ipc_peers, at::kLong, "ipc_peers");
+    check_dev(*ipc_arena, at::kLong, "ipc_arena");
+    check_dev(*ipc_epoch, at::kInt, "ipc_epoch");
+    check_dev(*ipc_err, at::kInt, "ipc_err");
+    TORCH_CHECK(ipc_peers->numel() == world, "bn_reduce_fused: peer table size");
+    TORCH_CHECK(ipc_epoch->numel() >= (C + 63) / 64, "bn_reduce_fused: epoch counters");
+    TORCH_CHECK(ipc_site >= 0 && ipc_site + bn_ipc_region_words((int)world, (int)S, (int)C) <=
+                                    ipc_arena->numel(),
+                "bn_reduce_fused: IPC site region outside the arena");
+    q.ipc_peers = reinterpret_cast<uint64_t* const*>(ipc_peers->data_ptr<int64_t>());
+    q.ipc_own = reinterpret_cast<uint64_t*>(ipc_arena->data_ptr<int64_t>());
+    q.ipc_site = ipc_site;
+    q.ipc_epoch = reinterpret_cast<unsigned*>(ipc_epoch->data_ptr<int>());
+    q.ipc_err = ipc_err->data_ptr<int>();
+    q.world = (int)world;
+    q.rank = (int)rank;
+  }
   bn_reduce_fused(q, cur_stream());
 }
 
@@ -727,7 +755,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
   m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
-  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0) -> ()", &bn_reduce_fused_op);
+  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0) -> ()", &bn_reduce_fused_op);
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);

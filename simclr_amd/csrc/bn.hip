@@ -171,9 +171,101 @@ struct BnReduceArgs {
   float* dgamma;
   float* dbeta;
   float* coef;
+  // IPC exchange (world > 1): see bn_ipc_exchange
+  uint64_t* const* peers;
+  uint64_t* own;
+  long long site;
+  unsigned* epoch;
+  int* err;
+  int world, rank;
 };
 
 constexpr int kMaxSeg = 4;  // BatchNorm segments (views) per launch handled by the reducer
+constexpr int kMaxWorld = 16;
+
+// Cross-rank sum of one channel group's [S][2][64] BatchNorm sums, replacing SyncBatchNorm's
+// all_gather / all_reduce (reference main.py:176 → torch/nn/modules/_functions.py:74,159) for
+// the latency-bound statistics exchange: no RCCL launch, no separate reduce / finalize kernels.
+// Every rank's arena (fine-grained, uncached device memory, mapped into every peer with
+// hipIpcOpenMemHandle) holds, per BatchNorm site, [parity][rank][2][S][C] 8-byte LL words:
+// the float's bits in the low half and the exchange epoch in the high half, so one 64-bit
+// store publishes value and flag together — no fence, no release/acquire, no L2 write-back
+// (the reader spins on each word until its epoch matches).  The last-arriving block of the
+// channel group pushes its slot to all ranks (system-scope relaxed stores through the peer
+// mappings), then waits for the W slots in its own arena and sums them in rank order, so every
+// rank finalizes from bitwise-identical statistics.  The epoch is a per-(site, group) counter
+// that advances once per call on every rank (SPMD order); parity double-buffers the region so
+// a rank running one call ahead never overwrites a slot a slower rank is still reading.  A
+// bounded spin sets *err and continues rather than hang the GPU if a peer never arrives.
+__device__ void bn_ipc_exchange(const BnReduceArgs& p, int cg, float (*fin)[2][64],
+                                unsigned* sh_epoch) {
+  const int S = p.S, C = p.C, W = p.world;
+  if (threadIdx.x == 0) {
+    const unsigned e = p.epoch[cg] + 1u;
+    p.epoch[cg] = e;
+    *sh_epoch = e;
+  }
+  __syncthreads();
+  const unsigned e = *sh_epoch;
+  const long long slot = 2LL * S * C;                 // words per rank slot
+  const long long base = p.site + (long long)(e & 1u) * W * slot;
+  const int nval = S * 2 * 64;                        // this group's values
+  // push: value v = (sg, k, cl) to word [k][sg][c] of slot `rank` in every arena
+  for (int i = threadIdx.x; i < W * nval; i += blockDim.x) {
+    const int r = i / nval, v = i - r * nval;
+    const int sg = v / 128, k = (v >> 6) & 1, cl = v & 63;
+    const int c = cg * 64 + cl;
+    if (c >= C) continue;
+    const uint64_t w = ((uint64_t)e << 32) | (uint64_t)__float_as_uint(fin[sg][k][cl]);
+    uint64_t* dst = p.peers[r] + base + (long long)p.rank * slot + (long long)k * S * C +
+                    (long long)sg * C + c;
+    __hip_atomic_store(dst, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // gather: every rank's word for this group, summed in rank order (identical on all ranks);
+  // all W loads of a value are in flight before the first is checked
+  static_assert(2 * kMaxSeg * 64 <= 2 * 256, "two values per thread at most");
+  float res[2] = {0.f, 0.f};
+  // wall-clock bound (100 MHz constant counter): 2 s per exchange, and none at all once an
+  // earlier exchange timed out — a lost peer costs seconds, never a hung GPU
+  const long long t0 = (long long)wall_clock64();
+  bool dead = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int v = threadIdx.x + j * 256;
+    const int sg = v / 128, k = (v >> 6) & 1, cl = v & 63;
+    const int c = cg * 64 + cl;
+    if (v >= nval || c >= C) continue;
+    const uint64_t* src = p.own + base + (long long)k * S * C + (long long)sg * C + c;
+    uint64_t w[kMaxWorld];
+#pragma unroll
+    for (int r = 0; r < kMaxWorld; ++r)
+      if (r < W) w[r] = __hip_atomic_load(src + r * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < kMaxWorld; ++r) {
+      if (r >= W) break;
+      while ((unsigned)(w[r] >> 32) != e) {
+        if (dead || (long long)wall_clock64() - t0 > 200000000LL) {
+          __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          dead = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        w[r] = __hip_atomic_load(src + r * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      a += __uint_as_float((uint32_t)w[r]);
+    }
+    res[j] = a;
+  }
+  __syncthreads();  // every thread done reading its local sums before fin is overwritten
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int v = threadIdx.x + j * 256;
+    const int sg = v / 128, k = (v >> 6) & 1, cl = v & 63;
+    if (v < nval && cg * 64 + cl < C) fin[sg][k][cl] = res[j];
+  }
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
   __shared__ float4 red4[kMaxSeg * 8][32];
@@ -266,9 +358,19 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
     f[0] = r.x; f[1] = r.y; f[2] = r.z; f[3] = r.w;
   }
   __syncthreads();
+  float dg = 0.f, db = 0.f;
+  if (p.world > 1 && p.mode != 0) {
+    // SyncBN semantics: dγ, dβ are per-rank (summed later by the gradient all-reduce), the
+    // normalisation statistics / input-gradient coefficients use the global sums
+    if (p.mode == 2 && lane == 0 && c < C)
+      for (int sg = 0; sg < S; ++sg) { db += fin[sg][0][cl]; dg += fin[sg][1][cl]; }
+    __shared__ unsigned sh_epoch;
+    bn_ipc_exchange(p, cg, fin, &sh_epoch);
+  }
   if (p.mode == 1 && c == 0 && lane == 0 && p.nbt != nullptr) p.nbt[0] += S;  // one per view
   if (lane != 0 || c >= C) return;
-  float rm = 0.f, rv = 0.f, dg = 0.f, db = 0.f, gm = 1.f;
+  float rm = 0.f, rv = 0.f, gm = 1.f;
+  const bool local_dgb = !(p.world > 1);
   if (p.mode == 1) {
     rm = p.running_mean ? p.running_mean[c] : 0.f;
     rv = p.running_var ? p.running_var[c] : 0.f;
@@ -295,8 +397,10 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
       rm = (1.f - p.momentum) * rm + p.momentum * mean;
       rv = (1.f - p.momentum) * rv + p.momentum * var * unbias;
     } else {
-      db += s1;
-      dg += s2;
+      if (local_dgb) {
+        db += s1;
+        dg += s2;
+      }
       const float mean = p.mi[sg * C + c], inv = p.mi[S * C + sg * C + c];
       const float A = gm * inv;
       const float bb = s1 / p.count, c2 = s2 / p.count;
@@ -866,6 +970,8 @@ void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s) {
   a.running_mean = q.running_mean; a.running_var = q.running_var; a.mi = q.mi; a.nbt = q.nbt;
   a.gamma = q.gamma; a.beta = q.beta; a.ss = q.ss;
   a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.coef = q.coef;
+  a.peers = q.ipc_peers; a.own = q.ipc_own; a.site = q.ipc_site; a.epoch = q.ipc_epoch;
+  a.err = q.ipc_err; a.world = q.world; a.rank = q.rank;
   hipLaunchKernelGGL(k_bn_reduce_fused, a.direct ? dim3((q.C + 63) / 64) : dim3((q.C + 63) / 64, q.S, a.G),
                      dim3(256), 0, s, a);
   HIP_CHECK_LAUNCH();

@@ -1,7 +1,7 @@
 """Build ``simclr_amd/_C.so`` in-tree with hipcc for gfx950 (no hipify, no JIT cache).
 
 The kernel translation units (``*.hip``) include only HIP headers and compile in parallel in a
-few seconds each; ``bindings.cpp`` is the only unit that sees the ATen headers.  Objects are
+few seconds each; ``bindings.cpp`` and ``ipc.cpp`` are the only units that see the ATen headers.  Objects are
 cached under ``csrc/_build`` and rebuilt when a source or a shared header is newer.
 
 Usage:  python -m simclr_amd.csrc.build [--force] [--jobs N] [--debug]
@@ -22,7 +22,7 @@ PKG = HERE.parent
 OUT = PKG / "_C.so"
 BUILD = HERE / "_build"
 KERNEL_SOURCES = ["conv.hip", "bn.hip", "misc.hip", "ntxent.hip", "lars.hip", "augment.hip"]
-BINDINGS = "bindings.cpp"
+BINDINGS = ["bindings.cpp", "ipc.cpp"]  # the units that see the ATen headers
 HEADERS = ["common.h", "kernels.h"]
 ARCH = os.environ.get("SIMCLR_OFFLOAD_ARCH", "gfx950")
 
@@ -70,13 +70,14 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
             tasks.append([hipcc, *common, "-c", str(s), "-o", str(o)])
     incs, libdirs, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    b = HERE / BINDINGS
-    bo = BUILD / "bindings.o"
-    objs.append(bo)
-    if force or _stale(bo, [b, *headers]):
-        tasks.append([hipcc, *common, "-x", "hip", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-                      f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *[f"-I{i}" for i in incs], f"-I{py_inc}",
-                      "-c", str(b), "-o", str(bo)])
+    for unit in BINDINGS:
+        b = HERE / unit
+        bo = BUILD / (b.stem + ".o")
+        objs.append(bo)
+        if force or _stale(bo, [b, *headers]):
+            tasks.append([hipcc, *common, "-x", "hip", "-D__HIP_PLATFORM_AMD__=1",
+                          "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                          *[f"-I{i}" for i in incs], f"-I{py_inc}", "-c", str(b), "-o", str(bo)])
     n = jobs or min(8, os.cpu_count() or 4)
     conv_rebuilt = any(str(BUILD / "conv.o") in t for t in tasks)
     if tasks:

@@ -115,8 +115,19 @@ struct BnReduceFusedParams {
   float* dgamma = nullptr;
   float* dbeta = nullptr;
   float* coef = nullptr;
+  // cross-rank exchange over IPC-mapped peer arenas (modes 1 / 2 at world > 1, see bn.hip)
+  uint64_t* const* ipc_peers = nullptr;  // device array [world] of arena bases (own included)
+  uint64_t* ipc_own = nullptr;           // this rank's arena base
+  long long ipc_site = 0;                // word offset of this BatchNorm's region
+  unsigned* ipc_epoch = nullptr;         // [ceil(C/64)] per-site exchange counters
+  int* ipc_err = nullptr;                // set on a spin timeout
+  int world = 1, rank = 0;
 };
 void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s);
+// words of one exchange region: 2 parities x world x [2][S][C] (LL words: value | epoch << 32)
+inline long long bn_ipc_region_words(int world, int S, int C) {
+  return 2LL * world * 2 * S * C;
+}
 // y = relu?(x*sc + sh + [res | res*rsc + rsh]); ss / rss are [2][S][C] scale/shift tables
 // optional mask: uint8 [R][C/8], bit e of byte (r, c/8) = (y[r][c] > 0)
 void bn_apply_ss(const uint16_t* x, const float* ss, const uint16_t* res, const float* rss,

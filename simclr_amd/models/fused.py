@@ -226,10 +226,14 @@ class FusedStages:
         Nb, H, W, C = xn.shape
         if H < getattr(self, "block_out_min_hw", 1):
             return False
-        g = fwd_geom(Nb, H, W, C, H, W, 1, 1, 1, 0, cs.conv.out_channels)
-        M = Nb * H * W
-        return any(ops.igemm_dual_ok(v, g) and (M // S) % ops.igemm_variant_bm(v) == 0
-                   for v in range(ops.igemm_nvariants()))
+        key = (Nb, H, W, C, cs.conv.out_channels, S)
+        cache = self.__dict__.setdefault("_dual_cache", {})
+        if key not in cache:  # host-side admissibility, once per shape
+            g = fwd_geom(Nb, H, W, C, H, W, 1, 1, 1, 0, cs.conv.out_channels)
+            M = Nb * H * W
+            cache[key] = any(ops.igemm_dual_ok(v, g) and (M // S) % ops.igemm_variant_bm(v) == 0
+                             for v in range(ops.igemm_nvariants()))
+        return cache[key]
 
     def _bn_fwd(self, ops, bn, partial, nblk_seg: int, rows_seg: int, S: int, st,
                 slot: int = 0) -> _BNState:
@@ -240,10 +244,14 @@ class FusedStages:
         count = float(rows_seg * st.world_size)
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ss = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        if not st.comm:  # one launch: reduce + finalize (last-arriver)
+        ipc = st.ipc
+        if not st.comm or ipc is not None:
+            # one launch: reduce + finalize (last-arriver); at world > 1 the IPC statistics
+            # exchange runs inside it (comm/ipc.py)
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
-                                bn.weight.detach(), bn.bias.detach(), ss, None, None, None, slot)
+                                bn.weight.detach(), bn.bias.detach(), ss, None, None, None, slot,
+                                **(ipc.kwargs((id(bn), "fwd"), S, C) if ipc is not None else {}))
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats, ticket_slot=slot)
@@ -279,8 +287,8 @@ class FusedStages:
         independent work (a weight gradient) before ``_bn_bwd_finish``.  Single GPU: nothing
         to wait for (one fused launch in the finish)."""
         C = bn.num_features
-        if not st.comm:
-            return ("local", bn, partial, nblk_seg, bs)
+        if not st.comm or st.ipc is not None:
+            return ("local", bn, partial, nblk_seg, bs, st.ipc)
         dev = partial.device
         sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, sums)
@@ -297,10 +305,13 @@ class FusedStages:
         dev = bs.mi.device
         coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
         if h[0] == "local":
-            partial, nblk_seg = h[2], h[3]
+            # single launch; with the IPC exchange dγ, dβ come from the local sums and coef
+            # from the global ones (SyncBN semantics, see _bn_bwd_start)
+            partial, nblk_seg, ipc = h[2], h[3], h[5]
+            kw = ipc.kwargs((id(bn), "bwd"), S, C) if ipc is not None else {}
             self._deliver_bn_grads(bn, lambda dg, db: ops.bn_reduce_fused(
                 partial, nblk_seg, S, C, 2, None, bs.count, 0.0, 0.0, None, None, bs.mi, None,
-                bn.weight.detach(), None, None, dg, db, coef))
+                bn.weight.detach(), None, None, dg, db, coef, **kw))
         else:
             sums, work = h[2], h[3]
             work.wait()

@@ -63,9 +63,11 @@ class BatchNormHipFn(torch.autograd.Function):
             ops.bn_stats(xr, S, partial)
         count = float((R // S) * st.world_size)
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        if not st.comm:
+        ipc = getattr(st, "ipc", None)
+        if not st.comm or ipc is not None:  # one launch (the IPC exchange runs inside it)
             ops.bn_reduce_fused(partial, nblk, S, C, 1, None, count, bn.eps, bn.momentum,
-                                bn.running_mean, bn.running_var, mi, bn.num_batches_tracked)
+                                bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
+                                **(ipc.kwargs((id(bn), "fwd"), S, C) if ipc is not None else {}))
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
             ops.bn_reduce_fused(partial, nblk, S, C, 0, stats)
@@ -78,6 +80,7 @@ class BatchNormHipFn(torch.autograd.Function):
         ctx.save_for_backward(x, y if relu else None, mi, weight)
         ctx.cfg = (S, relu, residual is not None, count, st)
         ctx.bias = bias
+        ctx.bn_key = id(bn)  # the BatchNorm's IPC exchange site (stable across steps)
         return y
 
     @staticmethod
@@ -99,9 +102,14 @@ class BatchNormHipFn(torch.autograd.Function):
         dgamma, gslot = _grad_out(weight)
         dbeta, bslot = _grad_out(ctx.bias)
         coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
-        if not st.comm:
+        ipc = getattr(st, "ipc", None)
+        if not st.comm or ipc is not None:
+            # with the IPC exchange the kernel writes dγ, dβ from the local sums and the
+            # coefficients from the global ones
             ops.bn_reduce_fused(partial, nblk, S, C, 2, None, count, 0.0, 0.0, None, None, mi,
-                                None, weight.detach(), None, None, dgamma, dbeta, coef)
+                                None, weight.detach(), None, None, dgamma, dbeta, coef,
+                                **(ipc.kwargs((ctx.bn_key, "bwd"), S, C) if ipc is not None
+                                   else {}))
         else:
             # dγ, dβ from the LOCAL sums (the data-parallel reducer sums them across ranks,
             # as SyncBatchNorm + DDP do); the input gradient needs the global sums

@@ -29,6 +29,9 @@ class ParallelState:
     # run every collective even at world_size 1 (a 1-rank RCCL group): exercises the
     # multi-GPU code path (comm streams, async handles, the stats communicator) on one GPU
     force_comm: bool = False
+    # one-shot IPC exchange of BatchNorm statistics (comm/ipc.py), replacing the statistics
+    # all-reduces at world > 1 when its self-test passed on every rank
+    ipc: Optional[object] = None
 
     @property
     def stats_group(self):

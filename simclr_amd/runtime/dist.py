@@ -64,10 +64,19 @@ def init_distributed(cfg=None, use_cuda: bool = True, backend: Optional[str] = N
                           backend=(dist.get_backend() if world > 1 else "none"))
     st.device = device
     pstate.make_stat_group(st)
+    if st.comm and device.type == "cuda":
+        # BatchNorm statistics over IPC-mapped peer memory (self-tested; RCCL otherwise)
+        from ..comm import setup_stats_exchange
+        setup_stats_exchange(st, device)
     return st
 
 
 def cleanup() -> None:
+    ipc = getattr(pstate.get(), "ipc", None)
+    if ipc is not None:
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()  # no peer still reads this rank's arena through its mapping
+        ipc.close()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     pstate.reset()

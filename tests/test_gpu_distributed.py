@@ -81,7 +81,7 @@ def _step(m, store, x, w):
         assert ex is not None and ex.calls == 1, "fused executor did not run"
 
 
-def _worker(rank, world, port, out, fused):
+def _worker(rank, world, port, out, fused, ipc=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dev = torch.device("cuda", 0)
@@ -92,6 +92,9 @@ def _worker(rank, world, port, out, fused):
                           backend="gloo")
     st.device = dev
     pstate.make_stat_group(st)
+    if ipc:  # BatchNorm statistics through the IPC-mapped arenas (both ranks on cuda:0)
+        from simclr_amd.comm import setup_stats_exchange
+        assert setup_stats_exchange(st, dev, "ipc") is not None
     m, store = _build(dev, fused)
     store.broadcast_from(0)
     v0, v1, w0, w1 = _inputs()
@@ -99,6 +102,8 @@ def _worker(rank, world, port, out, fused):
     x = torch.cat([v0[sl], v1[sl]]).to(dev)
     w = torch.cat([w0[sl], w1[sl]]).to(dev)
     _step(m, store, x, w)
+    if ipc:
+        assert not st.ipc.failed(), "IPC exchange timed out"
     zs = [torch.zeros_like(m._dbg_z) for _ in range(world)]
     dist.all_gather(zs, m._dbg_z)
     if rank == 0:
@@ -106,16 +111,19 @@ def _worker(rank, world, port, out, fused):
                     "rs": [b.float().cpu() for n, b in m.named_buffers() if "running" in n]},
                    out)
     dist.barrier()
+    if st.ipc is not None:
+        st.ipc.close()
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("fused", [False, True])
-def test_two_ranks_match_one_process(tmp_path, fused):
+@pytest.mark.parametrize("fused,ipc", [(False, False), (True, False), (False, True),
+                                       (True, True)])
+def test_two_ranks_match_one_process(tmp_path, fused, ipc):
     out = str(tmp_path / "r0.pt")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, out, fused))
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, out, fused, ipc))
              for r in range(WORLD)]
     for p in procs:
         p.start()

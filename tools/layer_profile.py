@@ -21,7 +21,7 @@ class _Timed:
 
     def __getattr__(self, name):
         f = getattr(self._real, name)
-        if not callable(f) or "variant" in name or name.endswith(("_bm", "_bn", "splits", "blocks")):
+        if not callable(f) or "variant" in name or name.endswith(("_bm", "_bn", "splits", "blocks", "_ok")):
             return f
 
         def wrap(*args, **kw):
