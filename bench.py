@@ -129,6 +129,11 @@ def run_ours(args, rank, world, dev):
     t1 = time.perf_counter()
     # host time spent issuing the steps (≈ wall time means the run is launch/CPU bound)
     args.host_issue_ms = host / args.steps * 1000.0
+    if st.ipc is not None and st.ipc.failed():  # a spin timed out: statistics were wrong
+        print(f"[bench] rank {rank}: IPC statistics exchange timed out", file=sys.stderr,
+              flush=True)
+        args.bn_comm = "ipc-timeout"
+
     return t1 - t0, float(loss.item()) if loss is not None else float("nan")
 
 

@@ -159,12 +159,17 @@ def setup_stats_exchange(st, device: torch.device, mode: Optional[str] = None):
     """Attach an IPC statistics exchange to the parallel state ``st`` when it applies.
 
     ``mode`` (or ``SIMCLR_BN_COMM``): ``rccl`` never, ``ipc`` always (raise if impossible),
-    ``auto`` (default) at world > 1 on GPUs when the self-test passes on every rank."""
+    ``auto`` (default) at world > 1 over RCCL (one GPU per rank) when the self-test passes on
+    every rank.  ``auto`` skips the gloo rehearsals that put several ranks on ONE GPU: their
+    processes' queues are time-sliced, so every exchange waits for a context switch (correct —
+    tests/test_gpu_distributed.py runs it explicitly — but ~50 ms per BatchNorm)."""
     mode = (mode or os.environ.get("SIMCLR_BN_COMM", "auto")).lower()
     st.ipc = None
     if mode == "rccl" or not st.comm or st.world_size < 2 or device.type != "cuda":
         if mode == "ipc" and st.world_size > 1 and device.type != "cuda":
             raise RuntimeError("SIMCLR_BN_COMM=ipc needs GPUs")
+        return None
+    if mode == "auto" and dist.get_backend(st.group) != "nccl":
         return None
     ex, ok = None, 0
     try:
