@@ -229,7 +229,8 @@ def main(argv=None):
     if bpath.exists():
         try:
             b = json.loads(bpath.read_text())
-            key = f"{args.model}-{_stem_key(args)}-b{args.batch}"
+            key = f"{args.model}-{_stem_key(args)}-b{args.batch}" + (
+                f"-s{args.size}" if args.size != 32 else "")
             per_gpu = b.get("images_per_sec_per_gpu", {}).get(key)
             if per_gpu:
                 base = per_gpu * world
@@ -247,8 +248,9 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": (round(value / base, 3) if (base and args.impl == "ours") else None),
         "dtype": args.precision if args.impl == "ours" else "fp32",
-        "data": "synthetic 32x32 uint8 CIFAR-shape images, random-init weights, on-device "
-                "SimCLR augmentation",
+        "data": (f"synthetic {args.size}x{args.size} uint8 "
+                 f"{'CIFAR' if args.size == 32 else 'ImageNet'}-shape images, random-init "
+                 "weights, on-device SimCLR augmentation"),
         "config": {
             "model": f"{args.model}-{_stem_label(args)}"
                      f"+projection-head({2048 if args.model == 'resnet50' else 512}-"

@@ -282,14 +282,156 @@ __global__ __launch_bounds__(AUG_THREADS) void k_augment(const uint8_t* __restri
   }
 }
 
+// ---- ImageNet-shape outputs (BASELINE config 5: 224x224) --------------------------------
+// The register-resident kernel above holds every output pixel of an image (<= 64x64) across
+// the colour ops, because contrast blends against the mean luma of the image as it is at that
+// point of the random op order.  For large outputs the block instead walks the pixels twice:
+// pass 1 recomputes crop + the ops before contrast and reduces the luma sum; pass 2 recomputes
+// them, applies contrast with the mean and the remaining ops and writes.  Every per-pixel op is
+// deterministic, so both passes see identical values (recompute instead of a scratch image).
+__device__ __forceinline__ void crop_pixel(const AugParams& P, const uint8_t* img, int W, int OH,
+                                           int OW, int p, float& r, float& g, float& b) {
+  const float sy = (float)P.ch / OH, sx = (float)P.cw / OW;
+  const int oy = p / OW;
+  int ox = p - oy * OW;
+  if (P.flip) ox = OW - 1 - ox;
+  float fy = (oy + 0.5f) * sy - 0.5f;
+  float fx = (ox + 0.5f) * sx - 0.5f;
+  fy = fminf(fmaxf(fy, 0.f), (float)(P.ch - 1));
+  fx = fminf(fmaxf(fx, 0.f), (float)(P.cw - 1));
+  const int y0 = (int)floorf(fy), x0 = (int)floorf(fx);
+  const int y1 = min(y0 + 1, P.ch - 1), x1 = min(x0 + 1, P.cw - 1);
+  const float wy = fy - y0, wx = fx - x0;
+  const uint8_t* p00 = img + ((size_t)(P.ci + y0) * W + (P.cj + x0)) * 3;
+  const uint8_t* p01 = img + ((size_t)(P.ci + y0) * W + (P.cj + x1)) * 3;
+  const uint8_t* p10 = img + ((size_t)(P.ci + y1) * W + (P.cj + x0)) * 3;
+  const uint8_t* p11 = img + ((size_t)(P.ci + y1) * W + (P.cj + x1)) * 3;
+  float c3[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float top = p00[c] + wx * (p01[c] - p00[c]);
+    const float bot = p10[c] + wx * (p11[c] - p10[c]);
+    const float v = top + wy * (bot - top);
+    c3[c] = fminf(fmaxf(floorf(v + 0.5f), 0.f), 255.f);
+  }
+  r = c3[0]; g = c3[1]; b = c3[2];
+}
+
+// one colour op (brightness / saturation / hue) on one pixel; contrast is handled by the caller
+__device__ __forceinline__ void pixel_op(const AugParams& P, int op, float& R, float& G,
+                                         float& B) {
+  if (op == 0) {
+    R = clip_trunc(R * P.fb); G = clip_trunc(G * P.fb); B = clip_trunc(B * P.fb);
+  } else if (op == 2) {
+    const float l = (float)luma(R, G, B);
+    R = clip_trunc(l + P.fs * (R - l));
+    G = clip_trunc(l + P.fs * (G - l));
+    B = clip_trunc(l + P.fs * (B - l));
+  } else if (op == 3) {
+    float h, s, v, r, g, bb;
+    rgb2hsv(R / 255.f, G / 255.f, B / 255.f, h, s, v);
+    h += P.fh;
+    h -= floorf(h);
+    hsv2rgb(h, s, v, r, g, bb);
+    R = fminf(fmaxf(floorf(r * 255.f + 0.5f), 0.f), 255.f);
+    G = fminf(fmaxf(floorf(g * 255.f + 0.5f), 0.f), 255.f);
+    B = fminf(fmaxf(floorf(bb * 255.f + 0.5f), 0.f), 255.f);
+  }
+}
+
+__global__ __launch_bounds__(AUG_THREADS) void k_augment_large(
+    const uint8_t* __restrict__ images, const int64_t* __restrict__ indices, int n, int H, int W,
+    int OH, int OW, int Cpad, float strength, uint64_t seed, uint64_t counter, int view_offset,
+    int flags, uint16_t* __restrict__ out, float* __restrict__ params_out) {
+  __shared__ AugParams P;
+  __shared__ long long red[AUG_THREADS / 64];
+  const int b = blockIdx.x, view = blockIdx.y + view_offset;
+  const int64_t idx = indices ? indices[b] : (int64_t)b;
+  const uint8_t* img = images + (size_t)idx * H * W * 3;
+  if (threadIdx.x == 0) {
+    if (flags & 1) {
+      Rng rng{splitmix64(seed ^ splitmix64(counter * 0x9E3779B97F4A7C15ull + (uint64_t)view) ^
+                         splitmix64((uint64_t)idx + 0x632BE59BD9B4E019ull)), 0};
+      sample_params(rng, H, W, strength, P);
+    } else {
+      P.ci = 0; P.cj = 0; P.ch = H; P.cw = W; P.flip = 0; P.jitter = 0; P.gray = 0;
+      P.fb = P.fc = P.fs = 1.f; P.fh = 0.f;
+      for (int i = 0; i < 4; ++i) P.order[i] = i;
+    }
+    if (params_out) {
+      float* po = params_out + ((size_t)blockIdx.y * n + b) * 16;
+      po[0] = P.ci; po[1] = P.cj; po[2] = P.ch; po[3] = P.cw; po[4] = P.flip; po[5] = P.jitter;
+      for (int i = 0; i < 4; ++i) po[6 + i] = P.order[i];
+      po[10] = P.fb; po[11] = P.fc; po[12] = P.fs; po[13] = P.fh; po[14] = P.gray; po[15] = 0.f;
+    }
+  }
+  __syncthreads();
+  const int npix = OH * OW;
+  int kc = 4;  // position of contrast in the op order (4: none / jitter off)
+  if (P.jitter)
+    for (int i = 0; i < 4; ++i)
+      if (P.order[i] == 1) kc = i;
+  float mean = 0.f;
+  if (kc < 4) {  // pass 1: mean luma of the image as contrast sees it
+    long long s = 0;
+    for (int p = threadIdx.x; p < npix; p += AUG_THREADS) {
+      float r, g, bb;
+      crop_pixel(P, img, W, OH, OW, p, r, g, bb);
+      for (int i = 0; i < kc; ++i) pixel_op(P, P.order[i], r, g, bb);
+      s += luma(r, g, bb);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    long long tot = 0;
+    for (int w = 0; w < AUG_THREADS / 64; ++w) tot += red[w];
+    mean = floorf((float)((double)tot / npix) + 0.5f);
+  }
+  const size_t obase = ((size_t)blockIdx.y * n + b) * npix;
+  const float inv255 = 1.f / 255.f;
+  for (int p = threadIdx.x; p < npix; p += AUG_THREADS) {  // pass 2
+    float r, g, bb;
+    crop_pixel(P, img, W, OH, OW, p, r, g, bb);
+    if (P.jitter)
+      for (int i = 0; i < 4; ++i) {
+        if (i == kc) {
+          r = clip_trunc(mean + P.fc * (r - mean));
+          g = clip_trunc(mean + P.fc * (g - mean));
+          bb = clip_trunc(mean + P.fc * (bb - mean));
+        } else {
+          pixel_op(P, P.order[i], r, g, bb);
+        }
+      }
+    if (P.gray) {
+      const float l = (float)luma(r, g, bb);
+      r = g = bb = l;
+    }
+    uint16_t* o = out + (obase + p) * Cpad;
+    if (Cpad == 8) {
+      u32x4 w;
+      w[0] = pack2bf(r * inv255, g * inv255);
+      w[1] = pack2bf(bb * inv255, 0.f);
+      w[2] = 0; w[3] = 0;
+      *(u32x4*)o = w;
+    } else {
+      o[0] = f2bf(r * inv255); o[1] = f2bf(g * inv255); o[2] = f2bf(bb * inv255);
+      for (int c = 3; c < Cpad; ++c) o[c] = 0;
+    }
+  }
+}
+
 }  // namespace
 
 void simclr_augment(const uint8_t* images, const int64_t* indices, int n, int views, int H, int W,
                     int OH, int OW, int Cpad, float strength, uint64_t seed, uint64_t counter,
                     int view_offset, int flags, uint16_t* out, float* params_out, hipStream_t s) {
-  if (OH * OW > AUG_THREADS * MAX_PIX_PER_THREAD) {
-    fprintf(stderr, "simclr_augment: output %dx%d too large\n", OH, OW);
-    abort();
+  if (OH * OW > AUG_THREADS * MAX_PIX_PER_THREAD) {  // two-pass kernel, any size
+    hipLaunchKernelGGL(k_augment_large, dim3(n, views), dim3(AUG_THREADS), 0, s, images, indices,
+                       n, H, W, OH, OW, Cpad, strength, seed, counter, view_offset, flags, out,
+                       params_out);
+    HIP_CHECK_LAUNCH();
+    return;
   }
   hipLaunchKernelGGL(k_augment, dim3(n, views), dim3(AUG_THREADS), 0, s, images, indices, n, H, W,
                      OH, OW, Cpad, strength, seed, counter, view_offset, flags, out, params_out);

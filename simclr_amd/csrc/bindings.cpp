@@ -731,9 +731,72 @@ void augment_op(const Tensor& images, const c10::optional<Tensor>& indices, int6
                  cur_stream());
 }
 
+// ---- eval.hip: maxpool (K2), cross-entropy + top-k (K10), centroid class sums (K11)
+void maxpool_fwd_op(const Tensor& x, const Tensor& y, const Tensor& arg, int64_t K, int64_t S,
+                    int64_t P) {
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4, "maxpool: NHWC 4-D tensors expected");
+  const int Nb = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  TORCH_CHECK(C % 8 == 0 && K >= 1 && K * K <= 255 && S >= 1 && P >= 0 && P < K,
+              "maxpool: C % 8 == 0, K*K <= 255, 0 <= P < K");
+  TORCH_CHECK(y.size(0) == Nb && y.size(1) == OH && y.size(2) == OW && y.size(3) == C,
+              "maxpool: output shape");
+  check_dev(arg, at::kByte, "arg");
+  TORCH_CHECK(arg.numel() == y.numel(), "maxpool: argmax size");
+  maxpool_fwd(bf(x, "x"), bfw(y, "y"), arg.data_ptr<uint8_t>(), Nb, H, W, C, OH, OW, (int)K,
+              (int)S, (int)P, cur_stream());
+}
+
+void maxpool_bwd_op(const Tensor& dy, const Tensor& arg, const Tensor& dx, int64_t K, int64_t S,
+                    int64_t P) {
+  TORCH_CHECK(dy.dim() == 4 && dx.dim() == 4, "maxpool_bwd: NHWC 4-D tensors expected");
+  const int Nb = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3);
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  TORCH_CHECK(C % 8 == 0 && K * K <= 255 && P < K, "maxpool_bwd: geometry");
+  TORCH_CHECK(dy.size(0) == Nb && dy.size(1) == OH && dy.size(2) == OW && dy.size(3) == C,
+              "maxpool_bwd: dy shape");
+  check_dev(arg, at::kByte, "arg");
+  TORCH_CHECK(arg.numel() == dy.numel(), "maxpool_bwd: argmax size");
+  maxpool_bwd(bf(dy, "dy"), arg.data_ptr<uint8_t>(), bfw(dx, "dx"), Nb, H, W, C, OH, OW, (int)K,
+              (int)S, (int)P, cur_stream());
+}
+
+void ce_topk_op(const Tensor& logits, const Tensor& y, double gscale, const Tensor& loss,
+                const Tensor& rank, const c10::optional<Tensor>& dlogits) {
+  TORCH_CHECK(logits.dim() == 2, "ce_topk: logits [B][C]");
+  const int B = logits.size(0), C = logits.size(1);
+  check_dev(y, at::kLong, "y");
+  check_dev(rank, at::kInt, "rank");
+  TORCH_CHECK(y.numel() == B && loss.numel() == B && rank.numel() == B, "ce_topk: row counts");
+  float* dl = optf32w(dlogits, "dlogits");
+  if (dl) TORCH_CHECK(dlogits->numel() == (int64_t)B * C, "ce_topk: dlogits size");
+  ce_topk(f32(logits, "logits"), y.data_ptr<int64_t>(), B, C, (float)gscale, f32w(loss, "loss"),
+          rank.data_ptr<int>(), dl, cur_stream());
+}
+
+void class_sums_op(const Tensor& X, const Tensor& y, int64_t NC, const Tensor& sums,
+                   const Tensor& counts) {
+  TORCH_CHECK(X.dim() == 2, "class_sums: X [N][D]");
+  const int N = X.size(0), D = X.size(1);
+  check_dev(y, at::kLong, "y");
+  TORCH_CHECK(y.numel() == N, "class_sums: labels");
+  TORCH_CHECK(NC >= 1 && class_sums_lds((int)NC) <= 64 * 1024, "class_sums: at most ~250 classes");
+  TORCH_CHECK(sums.numel() == NC * D && counts.numel() == NC, "class_sums: output sizes");
+  const int G = class_sums_groups(N);
+  at::Tensor part = at::empty({(int64_t)G * NC * D}, X.options());
+  at::Tensor pcnt = at::empty({(int64_t)G * NC}, X.options());
+  class_sums(f32(X, "X"), y.data_ptr<int64_t>(), N, D, (int)NC, part.data_ptr<float>(),
+             pcnt.data_ptr<float>(), f32w(sums, "sums"), f32w(counts, "counts"), cur_stream());
+}
+
 }  // namespace
 
+
 TORCH_LIBRARY(simclr_amd, m) {
+  m.def("maxpool_fwd(Tensor x, Tensor(a!) y, Tensor(b!) arg, int K, int S, int P) -> ()", &maxpool_fwd_op);
+  m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
+  m.def("ce_topk(Tensor logits, Tensor y, float gscale, Tensor(a!) loss, Tensor(b!) rank, Tensor(c!)? dlogits=None) -> ()", &ce_topk_op);
+  m.def("class_sums(Tensor X, Tensor y, int NC, Tensor(a!) sums, Tensor(b!) counts) -> ()", &class_sums_op);
   m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm);
   m.def("igemm_dual_ok(int v, int[] geom) -> bool", &igemm_dok);
   m.def("igemm_bm(int N) -> int", &igemm_bm);

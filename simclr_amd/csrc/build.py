@@ -21,7 +21,8 @@ HERE = Path(__file__).resolve().parent
 PKG = HERE.parent
 OUT = PKG / "_C.so"
 BUILD = HERE / "_build"
-KERNEL_SOURCES = ["conv.hip", "bn.hip", "misc.hip", "ntxent.hip", "lars.hip", "augment.hip"]
+KERNEL_SOURCES = ["conv.hip", "bn.hip", "misc.hip", "ntxent.hip", "lars.hip", "augment.hip",
+                  "eval.hip"]
 BINDINGS = ["bindings.cpp", "ipc.cpp"]  # the units that see the ATen headers
 HEADERS = ["common.h", "kernels.h"]
 ARCH = os.environ.get("SIMCLR_OFFLOAD_ARCH", "gfx950")

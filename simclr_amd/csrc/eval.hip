@@ -1,0 +1,233 @@
+// Remaining implicit kernels of the reference:
+//   K2  MaxPool2d(3, 2, 1) of the ImageNet stem (torchvision ResNet, reference model.py:90-92
+//       keeps it for resnet50 on 32x32 inputs) — NHWC bf16, forward records the window argmax
+//       (one byte per output element) so the backward is a deterministic gather, no atomics;
+//   K10 cross-entropy + top-k accuracy of the probes (reference eval.py:78,125-128) — one wave
+//       per row: online logsumexp, loss, optional dlogits = (softmax - onehot)·scale, and the
+//       target's rank (# classes scoring above it: top-k correct ⇔ rank < k, no sort);
+//   K11 centroid weights (reference model.py:44-52): per-class feature sums in one pass over
+//       the features, deterministic (each block owns a 64-column strip and walks every row).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------- maxpool
+// x [Nb][H][W][C] -> y [Nb][OH][OW][C], arg [Nb][OH][OW][C] (window tap 0..K*K-1); one thread
+// per (output pixel, 8-channel chunk), 16-byte loads
+__global__ void k_maxpool_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                              uint8_t* __restrict__ arg, int Nb, int H, int W, int C, int OH,
+                              int OW, int K, int S, int P) {
+  const int CH = C / 8;
+  const size_t total = (size_t)Nb * OH * OW * CH;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CH);
+    const size_t pix = i / CH;
+    const int ow = (int)(pix % OW);
+    const int oh = (int)((pix / OW) % OH);
+    const int n = (int)(pix / ((size_t)OW * OH));
+    float best[8];
+    int bt[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bt[e] = 0; }
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = oh * S - P + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int iw = ow * S - P + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const u32x4 v = *(const u32x4*)(x + (((size_t)n * H + ih) * W + iw) * C + cc * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (e & 1) ? hi_bf(v[e >> 1]) : lo_bf(v[e >> 1]);
+          // strict > keeps the first maximum in window order, like PyTorch's kernel; NaN wins
+          if (f > best[e] || f != f) { best[e] = f; bt[e] = kh * K + kw; }
+        }
+      }
+    }
+    u32x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = pack2bf(best[2 * e], best[2 * e + 1]);
+    *(u32x4*)(y + pix * C + cc * 8) = w;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a0 |= (uint32_t)bt[e] << (8 * e);
+      a1 |= (uint32_t)bt[e + 4] << (8 * e);
+    }
+    *(u32x2*)(arg + pix * C + cc * 8) = (u32x2){a0, a1};
+  }
+}
+
+// dx[n][ih][iw][c] = Σ over the output windows containing (ih, iw) whose argmax is this tap
+__global__ void k_maxpool_bwd(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                              uint16_t* __restrict__ dx, int Nb, int H, int W, int C, int OH,
+                              int OW, int K, int S, int P) {
+  const int CH = C / 8;
+  const size_t total = (size_t)Nb * H * W * CH;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CH);
+    const size_t pix = i / CH;
+    const int iw = (int)(pix % W);
+    const int ih = (int)((pix / W) % H);
+    const int n = (int)(pix / ((size_t)W * H));
+    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // oh such that oh*S - P <= ih <= oh*S - P + K - 1
+    const int oh0 = max(0, (ih + P - K + S) / S), oh1 = min(OH - 1, (ih + P) / S);
+    const int ow0 = max(0, (iw + P - K + S) / S), ow1 = min(OW - 1, (iw + P) / S);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const int kh = ih - (oh * S - P);
+      if (kh < 0 || kh >= K) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int kw = iw - (ow * S - P);
+        if (kw < 0 || kw >= K) continue;
+        const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + cc * 8;
+        const u32x2 a = *(const u32x2*)(arg + o);
+        const u32x4 v = *(const u32x4*)(dy + o);
+        const int tap = kh * K + kw;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int t = (int)(((e < 4 ? a[0] : a[1]) >> (8 * (e & 3))) & 0xffu);
+          if (t == tap) g[e] += (e & 1) ? hi_bf(v[e >> 1]) : lo_bf(v[e >> 1]);
+        }
+      }
+    }
+    u32x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = pack2bf(g[2 * e], g[2 * e + 1]);
+    *(u32x4*)(dx + pix * C + cc * 8) = w;
+  }
+}
+
+// ---------------------------------------------------------------------------- CE + top-k
+// logits [B][C] fp32, y [B] int64.  Per row: loss = lse - logit[y]; rank = #{j: logit[j] >
+// logit[y]} + #{j < y: logit[j] == logit[y]}; dlogits (optional) = (softmax - onehot)·gscale.
+// One 64-lane wave per row, 4 rows per block.
+__global__ __launch_bounds__(256) void k_ce_topk(const float* __restrict__ logits,
+                                                 const int64_t* __restrict__ y, int B, int C,
+                                                 float gscale, float* __restrict__ loss,
+                                                 int* __restrict__ rank,
+                                                 float* __restrict__ dlogits) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float* z = logits + (size_t)row * C;
+  const int t = (int)y[row];
+  const float zt = (t >= 0 && t < C) ? z[t] : NAN;
+  float m = -INFINITY, s = 0.f;
+  int above = 0;
+  for (int j = lane; j < C; j += 64) {
+    const float v = z[j];
+    above += (v > zt || (v == zt && j < t)) ? 1 : 0;
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; } else { s += __expf(v - m); }
+  }
+  // wave reduction of (m, s) and the count
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(s, off, 64);
+    const float mm = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+    m = mm;
+    above += __shfl_xor(above, off, 64);
+  }
+  const float lse = m + __logf(s);
+  if (lane == 0) {
+    loss[row] = lse - zt;
+    rank[row] = above;
+  }
+  if (dlogits != nullptr) {
+    float* d = dlogits + (size_t)row * C;
+    for (int j = lane; j < C; j += 64) d[j] = (__expf(z[j] - lse) - (j == t ? 1.f : 0.f)) * gscale;
+  }
+}
+
+// ---------------------------------------------------------------------------- centroid sums
+// X [N][D] fp32, y [N] int64 -> part [G][NC][D], pcnt [G][NC]: block (strip, g) owns a 64-column
+// strip and the rows r ≡ g (mod G), accumulating per-class sums in LDS in row order; then
+// k_class_sums_final adds the G partials in order (deterministic, no atomics).
+__global__ __launch_bounds__(64) void k_class_sums(const float* __restrict__ X,
+                                                   const int64_t* __restrict__ y, int N, int D,
+                                                   int NC, float* __restrict__ part,
+                                                   float* __restrict__ pcnt) {
+  extern __shared__ float acc[];  // [NC][64] + [NC]
+  const int cl = threadIdx.x, d = blockIdx.x * 64 + cl;
+  const int g = blockIdx.y, G = gridDim.y;
+  float* cnt = acc + (size_t)NC * 64;
+  for (int i = cl; i < NC * 64; i += 64) acc[i] = 0.f;
+  for (int i = cl; i < NC; i += 64) cnt[i] = 0.f;
+  __syncthreads();
+  for (int r = g; r < N; r += G) {
+    const int c = (int)y[r];
+    if (c < 0 || c >= NC) continue;
+    if (d < D) acc[c * 64 + cl] += X[(size_t)r * D + d];
+    if (cl == 0) cnt[c] += 1.f;
+  }
+  __syncthreads();
+  for (int c = 0; c < NC; ++c) {
+    if (d < D) part[((size_t)g * NC + c) * D + d] = acc[c * 64 + cl];
+  }
+  if (blockIdx.x == 0)
+    for (int c = cl; c < NC; c += 64) pcnt[(size_t)g * NC + c] = cnt[c];
+}
+
+__global__ void k_class_sums_final(const float* __restrict__ part, const float* __restrict__ pcnt,
+                                   int G, int NC, int D, float* __restrict__ sums,
+                                   float* __restrict__ counts) {
+  const size_t n = (size_t)NC * D;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + NC;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float a = 0.f;
+    if (i < n) {
+      for (int g = 0; g < G; ++g) a += part[(size_t)g * n + i];
+      sums[i] = a;
+    } else {
+      const size_t c = i - n;
+      for (int g = 0; g < G; ++g) a += pcnt[(size_t)g * NC + c];
+      counts[c] = a;
+    }
+  }
+}
+
+int grid_cap(size_t n) {
+  size_t b = (n + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
+}
+
+}  // namespace
+
+void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int Nb, int H, int W, int C,
+                 int OH, int OW, int K, int S, int P, hipStream_t s) {
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_cap((size_t)Nb * OH * OW * (C / 8))), dim3(256), 0,
+                     s, x, y, arg, Nb, H, W, C, OH, OW, K, S, P);
+  HIP_CHECK_LAUNCH();
+}
+
+void maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int Nb, int H, int W,
+                 int C, int OH, int OW, int K, int S, int P, hipStream_t s) {
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_cap((size_t)Nb * H * W * (C / 8))), dim3(256), 0, s,
+                     dy, arg, dx, Nb, H, W, C, OH, OW, K, S, P);
+  HIP_CHECK_LAUNCH();
+}
+
+void ce_topk(const float* logits, const int64_t* y, int B, int C, float gscale, float* loss,
+             int* rank, float* dlogits, hipStream_t s) {
+  hipLaunchKernelGGL(k_ce_topk, dim3((B + 3) / 4), dim3(256), 0, s, logits, y, B, C, gscale, loss,
+                     rank, dlogits);
+  HIP_CHECK_LAUNCH();
+}
+
+size_t class_sums_lds(int NC) { return ((size_t)NC * 64 + NC) * sizeof(float); }
+int class_sums_groups(int N) { return N >= 4096 ? 32 : 1; }
+
+void class_sums(const float* X, const int64_t* y, int N, int D, int NC, float* part, float* pcnt,
+                float* sums, float* counts, hipStream_t s) {
+  const int G = class_sums_groups(N);
+  hipLaunchKernelGGL(k_class_sums, dim3((D + 63) / 64, G), dim3(64), class_sums_lds(NC), s, X, y,
+                     N, D, NC, part, pcnt);
+  HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_class_sums_final, dim3(grid_cap((size_t)NC * D + NC)), dim3(256), 0, s, part,
+                     pcnt, G, NC, D, sums, counts);
+  HIP_CHECK_LAUNCH();
+}

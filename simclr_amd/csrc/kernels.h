@@ -192,3 +192,16 @@ void lr_schedule_step(int64_t* step, float* lr_out, double lr0, int64_t warmup, 
 void simclr_augment(const uint8_t* images, const int64_t* indices, int n, int views, int H, int W,
                     int OH, int OW, int Cpad, float strength, uint64_t seed, uint64_t counter,
                     int view_offset, int flags, uint16_t* out, float* params_out, hipStream_t s);
+
+// ---- eval.hip: maxpool (K2), cross-entropy + top-k (K10), centroid class sums (K11)
+void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int Nb, int H, int W, int C,
+                 int OH, int OW, int K, int S, int P, hipStream_t s);
+void maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int Nb, int H, int W,
+                 int C, int OH, int OW, int K, int S, int P, hipStream_t s);
+void ce_topk(const float* logits, const int64_t* y, int B, int C, float gscale, float* loss,
+             int* rank, float* dlogits, hipStream_t s);
+size_t class_sums_lds(int NC);
+int class_sums_groups(int N);
+void class_sums(const float* X, const int64_t* y, int N, int D, int NC, float* part, float* pcnt,
+                float* sums, float* counts, hipStream_t s);
+

@@ -102,15 +102,8 @@ class CentroidClassifier(nn.Module):
 
     @staticmethod
     def create_weights(dataset, num_classes: int) -> torch.Tensor:
-        """Per-class means as one segmented reduction (index_add) instead of C masked means."""
-        X = dataset.data
-        Y = dataset.targets.to(X.device).long()
-        sums = torch.zeros(num_classes, X.shape[1], dtype=torch.float64, device=X.device)
-        sums.index_add_(0, Y, X.double())
-        counts = torch.bincount(Y, minlength=num_classes).clamp_min(1).to(sums.dtype)
-        means = (sums / counts[:, None]).to(X.dtype)
-        # classes with no samples give NaN in the reference (mean of empty); keep that contract
-        empty = torch.bincount(Y, minlength=num_classes) == 0
-        if bool(empty.any()):
-            means[empty] = float("nan")
-        return means.t().contiguous()  # d x num_classes
+        """Per-class means as one segmented reduction (HIP class-sum kernel on the GPU, K11)
+        instead of C masked means; classes with no samples give NaN, as the reference's mean of
+        an empty selection."""
+        from ..ops.classify import class_means
+        return class_means(dataset.data, dataset.targets, num_classes).t().contiguous()

@@ -37,6 +37,7 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNorm2d, BatchNorm1d
 from ..ops.conv import Conv2d
+from ..ops.pooling import MaxPool2d
 from .heads import Linear
 
 
@@ -116,7 +117,7 @@ class ResNet(nn.Module):
         self.conv1 = Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool: nn.Module = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.maxpool: nn.Module = MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

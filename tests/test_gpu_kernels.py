@@ -233,6 +233,22 @@ def test_augment_matches_numpy(ops):
     assert same >= views * n - 1
 
 
+def test_augment_large_matches_numpy(ops):
+    """Outputs above 64x64 (ImageNet shape, BASELINE config 5) take the two-pass kernel."""
+    from simclr_amd.data import augment_ref
+    rng = np.random.default_rng(3)
+    S = 80
+    imgs = rng.integers(0, 256, size=(8, S, S, 3), dtype=np.uint8)
+    idx = np.arange(8, dtype=np.int64)
+    n, views = 8, 2
+    out = torch.empty((views * n, S, S, 8), device=DEV, dtype=torch.bfloat16)
+    ops.augment(torch.from_numpy(imgs).to(DEV), torch.from_numpy(idx).to(DEV), n, views, S, S, 8,
+                0.5, 7, 3, 0, 1, out, None)
+    ref = augment_ref.augment_batch(imgs, idx, views, S, S, 0.5, 7, 3)
+    got = out.float().cpu().numpy()[..., :3].transpose(0, 3, 1, 2)
+    assert np.mean(np.abs(got - ref) < 2.5 / 255 + 4e-3) > 0.97
+
+
 def test_augment_plain_mode(ops):
     rng = np.random.default_rng(1)
     imgs = torch.from_numpy(rng.integers(0, 256, size=(4, 32, 32, 3), dtype=np.uint8)).to(DEV)
