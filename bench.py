@@ -199,7 +199,11 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=512, help="images per GPU")
     ap.add_argument("--size", type=int, default=32)
     ap.add_argument("--precision", default="bf16")
-    ap.add_argument("--gather", action="store_true", help="global negatives (all-gather of z)")
+    ap.add_argument("--gather", dest="gather", action="store_true", default=None,
+                    help="global negatives: NT-Xent over the all-gathered embeddings of every "
+                         "rank (default at N > 1, the north star's loss)")
+    ap.add_argument("--local-loss", dest="gather", action="store_false",
+                    help="per-GPU NT-Xent, the reference's loss (loss.py has no collective)")
     ap.add_argument("--graph", action="store_true", default=None,
                     help="capture the step in a hipGraph (default: on)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
@@ -207,6 +211,8 @@ def main(argv=None):
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     args = ap.parse_args(argv)
     rank, world, local, dev = _init()
+    if args.gather is None:
+        args.gather = world > 1
     if args.graph is None:
         # the whole step, RCCL collectives included (thread-local capture mode), is one hipGraph
         # at every N: replays issue no per-kernel host work, so 8 ranks sharing the host CPUs

@@ -53,6 +53,16 @@ def nt_xent_torch(z: torch.Tensor, n: int, temperature: float, reduction: str = 
     return rows.sum() / n * 0.5
 
 
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """Per-device side stream of the gathered loss's collectives."""
+    if dev not in _SIDE:
+        _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return _SIDE[dev]
+
+
 class _NTXentHipFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, n, temperature, reduction, gather, st):
@@ -97,19 +107,33 @@ class _NTXentHipFn(torch.autograd.Function):
         Ccols = zall.shape[0]
         dev = zn.device
         g = gout.reshape(1).float().contiguous()
-        s_row = ops.nt_bwd_splits(R, Ccols)
-        part = torch.empty((s_row * R * D,), device=dev, dtype=torch.float32)
-        d_rows = torch.empty((R, D), device=dev, dtype=torch.float32)
-        ops.nt_backward_part(True, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part, s_row,
-                             d_rows)
         s_col = ops.nt_bwd_splits(Ccols, R)
         part2 = torch.empty((s_col * Ccols * D,), device=dev, dtype=torch.float32)
         d_cols = torch.empty((Ccols, D), device=dev, dtype=torch.float32)
         ops.nt_backward_part(False, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part2,
                              s_col, d_cols)
-        if gather and st.comm:
-            # only this rank's slice of the column gradient is needed: reduce-scatter moves
-            # 1/W of an all-reduce's bytes over the xGMI links
+        overlap = gather and st.comm and dev.type == "cuda"
+        if overlap:
+            # global negatives: only this rank's slice of the column gradient is needed, so a
+            # reduce-scatter (1/W of an all-reduce's bytes over xGMI) — issued on a side stream
+            # so it runs under the row-gradient kernel below
+            cur = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(cur)
+            mine = torch.empty((R, D), device=dev, dtype=torch.float32)
+            with torch.cuda.stream(side):
+                dist.reduce_scatter_tensor(mine, d_cols, group=st.group)
+            # (d_cols / mine stay referenced until the join below, which orders every later
+            # allocation on this stream after the side stream's use)
+        s_row = ops.nt_bwd_splits(R, Ccols)
+        part = torch.empty((s_row * R * D,), device=dev, dtype=torch.float32)
+        d_rows = torch.empty((R, D), device=dev, dtype=torch.float32)
+        ops.nt_backward_part(True, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part, s_row,
+                             d_rows)
+        if overlap:
+            cur.wait_stream(side)
+            d_rows += mine
+        elif gather and st.comm:
             mine = torch.empty((R, D), device=dev, dtype=torch.float32)
             dist.reduce_scatter_tensor(mine, d_cols, group=st.group)
             d_rows += mine
