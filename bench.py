@@ -116,17 +116,24 @@ def run_ours(args, rank, world, dev):
             tr.graph = None
             args.graph = False
     loss = None
-    for _ in range(args.warmup):
-        loss = tr.step(next_batch())
-    _sync(dev, world)
-    t0 = time.perf_counter()
-    host = 0.0
-    for _ in range(args.steps):
-        h0 = time.perf_counter()
-        loss = tr.step(next_batch())
-        host += time.perf_counter() - h0
-    _sync(dev, world)
-    t1 = time.perf_counter()
+    import contextlib
+    ctx = contextlib.nullcontext()
+    if os.environ.get("SIMCLR_HP_STREAM") == "1" and dev.type == "cuda" and not args.graph:
+        # experiment: the step's main stream at the highest priority (side streams stay low)
+        lo, hi = torch.cuda.Stream.priority_range()
+        ctx = torch.cuda.stream(torch.cuda.Stream(device=dev, priority=hi))
+    with ctx:
+        for _ in range(args.warmup):
+            loss = tr.step(next_batch())
+        _sync(dev, world)
+        t0 = time.perf_counter()
+        host = 0.0
+        for _ in range(args.steps):
+            h0 = time.perf_counter()
+            loss = tr.step(next_batch())
+            host += time.perf_counter() - h0
+        _sync(dev, world)
+        t1 = time.perf_counter()
     # host time spent issuing the steps (≈ wall time means the run is launch/CPU bound)
     args.host_issue_ms = host / args.steps * 1000.0
     if st.ipc is not None and st.ipc.failed():  # a spin timed out: statistics were wrong
