@@ -95,6 +95,89 @@ ConvFusion fusion_from(const c10::optional<Tensor>& pro_sc, const c10::optional<
   return f;
 }
 
+unsigned* tickets_for(const Tensor& like, int64_t n, int64_t slot);
+
+const float* tail_ptr(const std::vector<c10::optional<Tensor>>& t, size_t i, int64_t n,
+                      const char* name) {
+  if (i >= t.size() || !t[i].has_value() || !t[i]->defined()) return nullptr;
+  check_dev(*t[i], at::kFloat, name);
+  TORCH_CHECK(t[i]->numel() >= n, "igemm tail: ", name, " too small");
+  return t[i]->data_ptr<float>();
+}
+
+// BatchNorm finalize in the conv's last blocks (bn_tail.h).  tail_t = [mi, ss, rm, rv, nbt,
+// gamma, beta, dgamma, dbeta, coef, ipc_peers, ipc_arena, ipc_epoch, ipc_err], tail_f = [count,
+// eps, momentum], tail_i = [ipc_site, world, rank, ticket_slot].
+void set_tail(ConvFusion& f, const ConvGeom& g, int64_t M, int bm, int bn, const Tensor& stats,
+              int64_t stats_seg_blocks, int64_t epi_mode, const c10::optional<Tensor>& stats2,
+              int64_t mode, const std::vector<c10::optional<Tensor>>& t,
+              const std::vector<double>& tf, const std::vector<int64_t>& ti) {
+  TORCH_CHECK(mode == 1 || mode == 2, "igemm tail: mode 1 (forward) or 2 (backward)");
+  TORCH_CHECK(stats.defined() && stats.numel() > 0 && f.seg_rows > 0 && stats_seg_blocks == 0,
+              "igemm tail: needs the stats partials of one launch with seg_rows");
+  TORCH_CHECK(!(stats2.has_value() && stats2->defined()), "igemm tail: no second BN stream");
+  TORCH_CHECK((mode == 1 && epi_mode == 0) || (mode == 2 && (epi_mode == 3 || epi_mode == 4)),
+              "igemm tail: forward finalize after epilogue 0, backward after 3 / 4");
+  const int S = (int)(M / f.seg_rows);
+  TORCH_CHECK(S >= 1 && S <= 2 && g.N % 64 == 0 && f.seg_rows % bm == 0,
+              "igemm tail: <= 2 segments, channels % 64 == 0");
+  TORCH_CHECK(tf.size() == 3 && ti.size() == 4, "igemm tail: scalar lists");
+  const int64_t C = g.N, SC = (int64_t)S * C;
+  BnTailArgs& a = f.tail;
+  a.on = (int)mode;
+  a.nmb_seg = f.seg_rows / bm;
+  igemm_tail_plan(a.nmb_seg, &a.gr, &a.ngrp);
+  const int nNb = (g.N + bn - 1) / bn;
+  TORCH_CHECK(igemm_tail_ticket_words(nNb, S, a.ngrp) <= 4096, "igemm tail: ticket array");
+  BnFin& fin = a.fin;
+  fin.mode = (int)mode; fin.S = S; fin.C = (int)C;
+  fin.count = (float)tf[0]; fin.eps = (float)tf[1]; fin.momentum = (float)tf[2];
+  fin.mi = const_cast<float*>(tail_ptr(t, 0, 2 * SC, "mi"));
+  TORCH_CHECK(fin.mi != nullptr, "igemm tail: mi required");
+  if (mode == 1) {
+    fin.ss = const_cast<float*>(tail_ptr(t, 1, 2 * SC, "ss"));
+    fin.rm = const_cast<float*>(tail_ptr(t, 2, C, "running_mean"));
+    fin.rv = const_cast<float*>(tail_ptr(t, 3, C, "running_var"));
+    if (t.size() > 4 && t[4].has_value() && t[4]->defined()) {
+      check_dev(*t[4], at::kLong, "num_batches_tracked");
+      fin.nbt = t[4]->data_ptr<int64_t>();
+    }
+    fin.beta = tail_ptr(t, 6, C, "beta");
+  } else {
+    fin.dgamma = const_cast<float*>(tail_ptr(t, 7, C, "dgamma"));
+    fin.dbeta = const_cast<float*>(tail_ptr(t, 8, C, "dbeta"));
+    fin.coef = const_cast<float*>(tail_ptr(t, 9, 3 * SC, "coef"));
+    TORCH_CHECK(fin.coef != nullptr, "igemm tail: coef required");
+  }
+  fin.gamma = tail_ptr(t, 5, C, "gamma");
+  if (ti[1] > 1) {
+    TORCH_CHECK(t.size() == 14 && t[10].has_value() && t[11].has_value() && t[12].has_value() &&
+                    t[13].has_value(), "igemm tail: IPC exchange tensors");
+    const int64_t world = ti[1], rank = ti[2];
+    TORCH_CHECK(world <= 16 && rank >= 0 && rank < world, "igemm tail: world / rank");
+    check_dev(*t[10], at::kLong, "ipc_peers");
+    check_dev(*t[11], at::kLong, "ipc_arena");
+    check_dev(*t[12], at::kInt, "ipc_epoch");
+    check_dev(*t[13], at::kInt, "ipc_err");
+    TORCH_CHECK(t[10]->numel() == world && t[12]->numel() >= C / 64, "igemm tail: IPC tables");
+    TORCH_CHECK(ti[0] >= 0 && ti[0] + bn_ipc_region_words((int)world, S, (int)C) <= t[11]->numel(),
+                "igemm tail: IPC site outside the arena");
+    fin.ipc.peers = reinterpret_cast<uint64_t* const*>(t[10]->data_ptr<int64_t>());
+    fin.ipc.own = reinterpret_cast<uint64_t*>(t[11]->data_ptr<int64_t>());
+    fin.ipc.site = ti[0];
+    fin.ipc.epoch = reinterpret_cast<unsigned*>(t[12]->data_ptr<int>());
+    fin.ipc.err = t[13]->data_ptr<int>();
+    fin.ipc.world = (int)world;
+    fin.ipc.rank = (int)rank;
+  }
+  TORCH_CHECK(ti[3] >= 0 && ti[3] < 2, "igemm tail: ticket slot");
+  a.tick = tickets_for(stats, 4096, 2 + ti[3]);
+  // level-2 rows: only this launch uses them, on the current stream, so returning the block to
+  // the caching allocator right after the launch is safe (later users are stream-ordered)
+  at::Tensor ws = at::empty({(int64_t)S * a.ngrp * 2 * C}, stats.options().dtype(at::kFloat));
+  a.ws = ws.data_ptr<float>();
+}
+
 void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optional<Tensor>& bias,
            const c10::optional<Tensor>& stats, std::vector<int64_t> gv,
            const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
@@ -107,7 +190,9 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const c10::optional<Tensor>& epi_mi2, const c10::optional<Tensor>& stats2,
            const c10::optional<Tensor>& pro_d, const c10::optional<Tensor>& A2,
            const c10::optional<Tensor>& pro_rss, const c10::optional<Tensor>& pro_out,
-           const c10::optional<Tensor>& pro_mask) {
+           const c10::optional<Tensor>& pro_mask, int64_t tail_mode,
+           const std::vector<c10::optional<Tensor>>& tail_t, std::vector<double> tail_f,
+           std::vector<int64_t> tail_i) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -225,8 +310,28 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
       f.pro_rsh = f.pro_rsc + nseg * g.C;
     }
   }
+  if (tail_mode != 0) set_tail(f, g, M, bm, igemm_variant_bn((int)variant), has_stats ? *stats : out, stats_seg_blocks, epi_mode,
+                               stats2, tail_mode, tail_t, tail_f, tail_i);
   conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
                 optf32w(stats, "stats"), f, (int)variant, cur_stream());
+}
+
+void igemm_plain(const Tensor& A, const Tensor& B, const Tensor& out,
+                 const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
+                 std::vector<int64_t> gv, const c10::optional<Tensor>& pro_sc,
+                 const c10::optional<Tensor>& pro_sh, int64_t pro_seg_rows, bool pro_relu,
+                 int64_t epi_mode, const c10::optional<Tensor>& epi_a,
+                 const c10::optional<Tensor>& epi_b, int64_t variant,
+                 const c10::optional<Tensor>& epi_ss, const c10::optional<Tensor>& epi_mi,
+                 int64_t seg_rows, int64_t stats_seg_blocks, int64_t stats_base,
+                 const c10::optional<Tensor>& epi_c, const c10::optional<Tensor>& epi_mask,
+                 const c10::optional<Tensor>& epi_c2, const c10::optional<Tensor>& epi_mi2,
+                 const c10::optional<Tensor>& stats2, const c10::optional<Tensor>& pro_d,
+                 const c10::optional<Tensor>& A2, const c10::optional<Tensor>& pro_rss,
+                 const c10::optional<Tensor>& pro_out, const c10::optional<Tensor>& pro_mask) {
+  igemm(A, B, out, bias, stats, std::move(gv), pro_sc, pro_sh, pro_seg_rows, pro_relu, epi_mode,
+        epi_a, epi_b, variant, epi_ss, epi_mi, seg_rows, stats_seg_blocks, stats_base, epi_c,
+        epi_mask, epi_c2, epi_mi2, stats2, pro_d, A2, pro_rss, pro_out, pro_mask, 0, {}, {}, {});
 }
 
 int64_t igemm_bm(int64_t N) { return igemm_block_m((int)N); }
@@ -407,7 +512,7 @@ void bn_final(const Tensor& stats, int64_t S, int64_t C, double count, double ep
 
 // persistent zeroed ticket arrays for the last-arriver reductions, per device and per slot:
 // reductions that may run concurrently (different streams) must use different slots
-constexpr int kTicketSlots = 2;
+constexpr int kTicketSlots = 4;  // 0/1 BN reduce per stream, 2/3 conv tails per stream
 constexpr int64_t kTicketStride = 4096;
 unsigned* tickets_for(const Tensor& like, int64_t n, int64_t slot) {
   static std::vector<Tensor> per_dev;
@@ -502,6 +607,8 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
     q.world = (int)world;
     q.rank = (int)rank;
   }
+  static const bool skip_for_timing = getenv("SIMCLR_EXPERIMENT_SKIP_BNRED") != nullptr;
+  if (skip_for_timing) return;  // timing experiment only: statistics left stale
   bn_reduce_fused(q, cur_stream());
 }
 
@@ -797,7 +904,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
   m.def("ce_topk(Tensor logits, Tensor y, float gscale, Tensor(a!) loss, Tensor(b!) rank, Tensor(c!)? dlogits=None) -> ()", &ce_topk_op);
   m.def("class_sums(Tensor X, Tensor y, int NC, Tensor(a!) sums, Tensor(b!) counts) -> ()", &class_sums_op);
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm_plain);
+  m.def("igemm_t(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc, Tensor? pro_sh, int pro_seg_rows, bool pro_relu, int epi_mode, Tensor? epi_a, Tensor? epi_b, int variant, Tensor? epi_ss, Tensor? epi_mi, int seg_rows, int stats_seg_blocks, int stats_base, Tensor? epi_c, Tensor? epi_mask, Tensor? epi_c2, Tensor? epi_mi2, Tensor(c!)? stats2, Tensor? pro_d, Tensor? A2, Tensor? pro_rss, Tensor(d!)? pro_out, Tensor(e!)? pro_mask, int tail_mode, Tensor(f!)?[] tail_t, float[] tail_f, int[] tail_i) -> ()", &igemm);
   m.def("igemm_dual_ok(int v, int[] geom) -> bool", &igemm_dok);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);

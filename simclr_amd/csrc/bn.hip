@@ -240,21 +240,27 @@ __device__ void bn_ipc_exchange(const BnReduceArgs& p, int cg, float (*fin)[2][6
 #pragma unroll
     for (int r = 0; r < kMaxWorld; ++r)
       if (r < W) w[r] = __hip_atomic_load(src + r * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // poll every pending slot per round (unrolled rank loop: w stays in registers)
+    while (true) {
+      bool pending = false;
+#pragma unroll
+      for (int r = 0; r < kMaxWorld; ++r)
+        if (r < W && (unsigned)(w[r] >> 32) != e) {
+          pending = true;
+          w[r] = __hip_atomic_load(src + r * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      if (!pending) break;
+      if (dead || (long long)wall_clock64() - t0 > 200000000LL) {
+        __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dead = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
     float a = 0.f;
 #pragma unroll
-    for (int r = 0; r < kMaxWorld; ++r) {
-      if (r >= W) break;
-      while ((unsigned)(w[r] >> 32) != e) {
-        if (dead || (long long)wall_clock64() - t0 > 200000000LL) {
-          __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          dead = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        w[r] = __hip_atomic_load(src + r * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      a += __uint_as_float((uint32_t)w[r]);
-    }
+    for (int r = 0; r < kMaxWorld; ++r)
+      if (r < W) a += __uint_as_float((uint32_t)w[r]);
     res[j] = a;
   }
   __syncthreads();  // every thread done reading its local sums before fin is overwritten
@@ -267,6 +273,9 @@ __device__ void bn_ipc_exchange(const BnReduceArgs& p, int cg, float (*fin)[2][6
   __syncthreads();
 }
 
+// IPC: the cross-rank exchange is compiled only into the world > 1 instantiation, so the
+// single-GPU kernel keeps its small register / argument footprint
+template <bool IPC>
 __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
   __shared__ float4 red4[kMaxSeg * 8][32];
   __shared__ float fin[kMaxSeg][2][64];
@@ -359,7 +368,7 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
   }
   __syncthreads();
   float dg = 0.f, db = 0.f;
-  if (p.world > 1 && p.mode != 0) {
+  if (IPC && p.world > 1 && p.mode != 0) {
     // SyncBN semantics: dγ, dβ are per-rank (summed later by the gradient all-reduce), the
     // normalisation statistics / input-gradient coefficients use the global sums
     if (p.mode == 2 && lane == 0 && c < C)
@@ -370,7 +379,7 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
   if (p.mode == 1 && c == 0 && lane == 0 && p.nbt != nullptr) p.nbt[0] += S;  // one per view
   if (lane != 0 || c >= C) return;
   float rm = 0.f, rv = 0.f, gm = 1.f;
-  const bool local_dgb = !(p.world > 1);
+  const bool local_dgb = !(IPC && p.world > 1);
   if (p.mode == 1) {
     rm = p.running_mean ? p.running_mean[c] : 0.f;
     rv = p.running_var ? p.running_var[c] : 0.f;
@@ -972,8 +981,11 @@ void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s) {
   a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.coef = q.coef;
   a.peers = q.ipc_peers; a.own = q.ipc_own; a.site = q.ipc_site; a.epoch = q.ipc_epoch;
   a.err = q.ipc_err; a.world = q.world; a.rank = q.rank;
-  hipLaunchKernelGGL(k_bn_reduce_fused, a.direct ? dim3((q.C + 63) / 64) : dim3((q.C + 63) / 64, q.S, a.G),
-                     dim3(256), 0, s, a);
+  const dim3 grid = a.direct ? dim3((q.C + 63) / 64) : dim3((q.C + 63) / 64, q.S, a.G);
+  if (a.world > 1 && a.peers != nullptr)
+    hipLaunchKernelGGL(k_bn_reduce_fused<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_bn_reduce_fused<false>, grid, dim3(256), 0, s, a);
   HIP_CHECK_LAUNCH();
 }
 

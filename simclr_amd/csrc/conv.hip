@@ -26,6 +26,7 @@
 // with an XOR chunk swizzle (cdna_hip_programming.md T2), XCD-aware block remap (T1).
 #include "common.h"
 #include "kernels.h"
+#include "bn_tail.h"
 
 namespace {
 
@@ -79,6 +80,8 @@ struct IgemmArgs {
   // stats row remap (segment-major partials when one BN's rows span several launches):
   //   blk = seg * stats_seg_blocks + stats_base + (m0 - seg * seg_rows) / BM, seg = m0 / seg_rows
   int seg_rows, stats_seg_blocks, stats_base;
+  // BatchNorm finalize in this launch's last blocks (igemm_bn_tail; on == 0: partials only)
+  BnTailArgs tail;
 };
 
 __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const float* sh, bool ok,
@@ -178,6 +181,103 @@ __device__ __forceinline__ void epi_load_batch(const IgemmArgs& p, int m0, int n
 // overlaps the operand DMA of the (short-K) GEMM instead of following it.
 template <int EPI>
 constexpr bool epi_prefetch() { return EPI == 4 || EPI == 5; }
+
+// BatchNorm finalize in the last blocks of the launch (bn_tail.h): the last of every level-1
+// group of `gr` row-blocks (same segment, same channel tile) sums the group's partial rows; the
+// last of those per channel tile sums the groups of every segment, runs the cross-rank exchange
+// (world > 1) and finalizes the tile's channels.  Fixed summation order: deterministic.
+template <int BM, int BN, int NT>
+__device__ void igemm_bn_tail(const IgemmArgs& p, int m0, int n0, int mb, char* smem) {
+  const BnTailArgs& t = p.tail;
+  const int S = t.fin.S, N = p.N, tid = threadIdx.x;
+  const int nb = n0 / BN;
+  const int seg = m0 / p.seg_rows;
+  const int local = mb - seg * t.nmb_seg;
+  const int grp = local / t.gr;
+  const int gbeg = grp * t.gr, gend = min(t.nmb_seg, gbeg + t.gr);
+  int* flag = (int*)smem;
+  unsigned* sh_ep = (unsigned*)smem + 4;
+  float* v = (float*)smem + 16;  // [S][2][BN]
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partial row has landed
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* tk = t.tick + ((size_t)nb * S + seg) * t.ngrp + grp;
+    const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(gend - gbeg - 1);
+    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // level 1: the group's rows of this channel tile
+  for (int q = tid; q < 2 * BN; q += NT) {
+    const int k = q / BN, j = q - k * BN, n = n0 + j;
+    if (n >= N) continue;
+    const float* src = p.stats + ((size_t)(seg * t.nmb_seg) * 2 + k) * N + n;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = gbeg;
+    for (; r + 3 < gend; r += 4) {
+      a0 += src[(size_t)r * 2 * N];
+      a1 += src[(size_t)(r + 1) * 2 * N];
+      a2 += src[(size_t)(r + 2) * 2 * N];
+      a3 += src[(size_t)(r + 3) * 2 * N];
+    }
+    for (; r < gend; ++r) a0 += src[(size_t)r * 2 * N];
+    __hip_atomic_store(&t.ws[(((size_t)seg * t.ngrp + grp) * 2 + k) * N + n], (a0 + a1) + (a2 + a3),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* tk = t.tick + (size_t)p.nNb * S * t.ngrp + nb;
+    const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(S * t.ngrp - 1);
+    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // level 2: every segment's group sums of this channel tile, in group order
+  for (int q = tid; q < S * 2 * BN; q += NT) {
+    const int sk = q / BN, j = q - sk * BN, n = n0 + j;
+    float a = 0.f;
+    if (n < N)
+      for (int g = 0; g < t.ngrp; ++g)
+        a += t.ws[(((size_t)(sk >> 1) * t.ngrp + g) * 2 + (sk & 1)) * N + n];
+    v[q] = a;
+  }
+  __syncthreads();
+  float l1[kTailMaxS], l2[kTailMaxS];  // rank-local sums (dγ, dβ)
+  if (tid < BN) {
+#pragma unroll
+    for (int sg = 0; sg < kTailMaxS; ++sg) {
+      l1[sg] = sg < S ? v[(sg * 2) * BN + tid] : 0.f;
+      l2[sg] = sg < S ? v[(sg * 2 + 1) * BN + tid] : 0.f;
+    }
+  }
+  if (t.fin.ipc.peers != nullptr && t.fin.ipc.world > 1)
+    tail_ipc_exchange(t.fin.ipc, S, N, n0, BN, v, sh_ep);
+  if (tid < BN && n0 + tid < N) {
+    float g1[kTailMaxS], g2[kTailMaxS];
+#pragma unroll
+    for (int sg = 0; sg < kTailMaxS; ++sg) {
+      g1[sg] = sg < S ? v[(sg * 2) * BN + tid] : 0.f;
+      g2[sg] = sg < S ? v[(sg * 2 + 1) * BN + tid] : 0.f;
+    }
+    bn_fin_col(t.fin, n0 + tid, g1, g2, l1, l2);
+  }
+  if (t.fin.mode == 1 && nb == 0 && tid == 0 && t.fin.nbt != nullptr) t.fin.nbt[0] += S;
+}
 
 // Epilogue shared by the igemm kernels: bias, bf16 round, LDS-staged 16-B row stores, fused
 // elementwise modes 1-5 and the per-block BatchNorm partial statistics (see IgemmArgs).
@@ -355,13 +455,27 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
       const int blk = p.stats_seg_blocks > 0
                           ? seg * p.stats_seg_blocks + p.stats_base + (m0 - seg * p.seg_rows) / BM
                           : mb;
-      p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
-      p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
+      if (p.tail.on) {
+        // write-through (agent-scope) stores: this kernel's tail may read them from another
+        // XCD (bn_tail.h); a separate reduce kernel sees plain stores at the kernel boundary
+        __hip_atomic_store(&p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid], a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid], b, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
+        p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
+      }
       if (two) {
         p.stats2[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
         p.stats2[((size_t)blk * 2 + 1) * p.N + n0 + tid] = d;
       }
     }
+#ifndef SIMCLR_NO_BN_TAIL
+    if (EPI == 0 || EPI == 3 || EPI == 4) {
+      if (p.tail.on) igemm_bn_tail<BM, BN, NT>(p, m0, n0, mb, smem);
+    }
+#endif
   }
 }
 
@@ -1869,6 +1983,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_c2 = f.epi_c2; a.epi_mi2 = f.epi_mi2; a.stats2 = f.stats2;
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
+  a.tail = f.tail;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
   if (a.pro_out != nullptr
           ? !igemm_dual_ok(variant, g)
@@ -1897,6 +2012,14 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     default: launch_igemm<64, 64, 2, 2>(a, s); break;
   }
 }
+
+void igemm_tail_plan(int nmb_seg, int* gr, int* ngrp) {
+  int g = 32;
+  while ((nmb_seg + g - 1) / g > 64) g *= 2;  // <= 64 level-2 rows per segment
+  *gr = g;
+  *ngrp = (nmb_seg + g - 1) / g;
+}
+int igemm_tail_ticket_words(int nNb, int S, int ngrp) { return nNb * S * ngrp + nNb; }
 
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }

@@ -17,6 +17,40 @@ struct ConvGeom {
 };
 
 // ---- conv.hip
+// BatchNorm finalize in the conv kernel's tail (bn_tail.h): cross-rank exchange + finalize
+// parameters, and the two-level last-arriver plan over the launch's row-blocks.
+struct IpcX {
+  uint64_t* const* peers = nullptr;  // [world] arena bases (own included); nullptr = no exchange
+  uint64_t* own = nullptr;
+  long long site = 0;                // word offset of this BatchNorm's region
+  unsigned* epoch = nullptr;         // per-64-channel-group counters of the site
+  int* err = nullptr;
+  int world = 1, rank = 0;
+};
+struct BnFin {
+  int mode = 0;  // 1 forward finalize, 2 backward finalize
+  int S = 1, C = 0;
+  float count = 1.f, eps = 1e-5f, momentum = 0.1f;
+  float* rm = nullptr;
+  float* rv = nullptr;
+  float* mi = nullptr;         // mode 1 out / mode 2 in: [2][S][C] mean, invstd
+  int64_t* nbt = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float* ss = nullptr;         // mode 1 out: [2][S][C] scale, shift
+  float* dgamma = nullptr;     // mode 2 out (rank-local sums)
+  float* dbeta = nullptr;
+  float* coef = nullptr;       // mode 2 out: [3][S][C]
+  IpcX ipc;
+};
+struct BnTailArgs {
+  int on = 0;                  // 0 off, else fin.mode
+  int nmb_seg = 0;             // row-blocks per segment (seg_rows / BM)
+  int gr = 1, ngrp = 1;        // level-1 group size (row-blocks) and groups per segment
+  unsigned* tick = nullptr;    // [nNb][S][ngrp] level-1 + [nNb] level-2 (zeroed, self-resetting)
+  float* ws = nullptr;         // level-2 rows [S][ngrp][2][N]
+  BnFin fin;
+};
 // Optional fusions around the implicit GEMM (all pointers nullable / mode 0 = off).
 struct ConvFusion {
   const float* pro_sc = nullptr;  // A/X-operand prologue: a = relu?(x*sc[seg][c] + sh[seg][c])
@@ -49,7 +83,11 @@ struct ConvFusion {
   int seg_rows = 0;               // rows per segment of the output (stats remap, mode 3)
   int stats_seg_blocks = 0;       // >0: segment-major stats rows (see conv.hip)
   int stats_base = 0;
+  BnTailArgs tail;                // BatchNorm finalize in the kernel's last blocks (bn_tail.h)
 };
+int igemm_tail_ticket_words(int nNb, int S, int ngrp);
+void igemm_tail_plan(int nmb_seg, int* gr, int* ngrp);
+
 int igemm_num_variants();
 int igemm_variant_bm(int v);
 int igemm_variant_bn(int v);

@@ -142,6 +142,11 @@ class FusedStages:
         v = os.environ.get("SIMCLR_BLOCK_OUT_PROLOGUE", "1")
         self.block_out_min_hw = int(v) if v.isdigit() else 1
         self.block_out_prologue = self.block_out_min_hw > 0
+        # BatchNorm reduce + finalize in the producing conv kernel's last blocks (csrc/bn_tail.h)
+        # instead of a separate reduce launch per BatchNorm.  Off by default: every block then
+        # has to drain its stores (incl. the nontemporal output tile) before its ticket, which
+        # costs more than the launches it saves (24.33 -> 25.59 ms/step A/B, r2 log)
+        self.bn_tail = os.environ.get("SIMCLR_BN_TAIL", "0") == "1"
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -189,13 +194,36 @@ class FusedStages:
         return True
 
     # ------------------------------------------------------------------ building blocks
+    def _tail_ok(self, st, C: int, S: int) -> bool:
+        return (getattr(self, "bn_tail", False) and C % 64 == 0 and S <= 2
+                and (not st.comm or st.ipc is not None))
+
+    def _tail_spec(self, bn, mode: int, S: int, st, slot: int, count: float, mi, ss=None,
+                   dgamma=None, dbeta=None, coef=None):
+        """(mode, tensors, floats, ints) of a conv-tail BatchNorm finalize (ops/conv_hip.py)."""
+        C = bn.num_features
+        t = [mi, ss,
+             bn.running_mean if mode == 1 else None, bn.running_var if mode == 1 else None,
+             bn.num_batches_tracked if mode == 1 else None,
+             bn.weight.detach(), bn.bias.detach() if mode == 1 else None, dgamma, dbeta, coef]
+        ints = [0, 1, 0, slot]
+        if st.ipc is not None:
+            kw = st.ipc.kwargs((id(bn), "fwd" if mode == 1 else "bwd"), S, C)
+            t += [kw["ipc_peers"], kw["ipc_arena"], kw["ipc_epoch"], kw["ipc_err"]]
+            ints = [kw["ipc_site"], kw["world"], kw["rank"], slot]
+        return (mode, t, [count, bn.eps if mode == 1 else 0.0,
+                          bn.momentum if mode == 1 else 0.0], ints)
+
     def _conv_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int,
-                  dual=None):
+                  dual=None, st=None, slot: int = 0):
         """a = conv(pro(x)) with BN statistics partials in the epilogue.
 
         ``dual = (aL, ss, res, rss, out, mask)``: the input is the previous block's output,
         formed in this conv's prologue from that block's conv3 activation ``aL`` and residual
-        ``res`` and written to ``out`` / ``mask`` by the same kernel (``xn`` is ``out``)."""
+        ``res`` and written to ``out`` / ``mask`` by the same kernel (``xn`` is ``out``).
+        Returns (a, partials, blocks per segment, bn state): with ``st`` given and the conv
+        tail applicable, the conv's last blocks also finalize ``cs.bn`` (state returned,
+        partials None); otherwise the caller reduces the partials (``_bn_fwd``)."""
         Nb, H, W, C = xn.shape
         Co = cs.conv.out_channels
         OH = (H + 2 * cs.pad - cs.k) // cs.stride + 1
@@ -214,8 +242,17 @@ class FusedStages:
         v = igemm_choose(ops, A, w, a, g, want_stats=True, pro=pro, seg_rows=M // S, dual=dl)
         bm = ops.igemm_variant_bm(v)
         stats = torch.empty(((M // bm) * 2 * Co,), device=xn.device, dtype=torch.float32)
-        igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl)
-        return a, stats, M // bm // S
+        tail, bs = None, None
+        if st is not None and self._tail_ok(st, Co, S):
+            bn = cs.bn
+            mi = torch.empty((2 * S * Co,), device=xn.device, dtype=torch.float32)
+            ss = torch.empty((2 * S * Co,), device=xn.device, dtype=torch.float32)
+            count = float((M // S) * st.world_size)
+            tail = self._tail_spec(bn, 1, S, st, slot, count, mi, ss=ss)
+            bs = _BNState(mi, ss.view(2, S * Co), count)
+        igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl, tail=tail,
+                     seg_rows=M // S if tail is not None else 0)
+        return a, stats, M // bm // S, bs
 
     def _dual_ok(self, ops, xn, cs: _ConvSpec, S: int) -> bool:
         """Can ``cs`` (a block's conv1) form its input — the previous block's output — in its
@@ -261,6 +298,25 @@ class FusedStages:
                             bn.bias.detach(), ss)
         return _BNState(mi, ss.view(2, S * C), count)
 
+    def _bn_grad_targets(self, bn):
+        """(dγ out, dβ out, finish): the flat-store slots (finish marks them ready for the
+        bucketed all-reduce) or temporaries handed to ``_deliver_grad`` by finish."""
+        gslot = getattr(bn.weight, "_slot", None)
+        bslot = getattr(bn.bias, "_slot", None)
+        if gslot is not None and bslot is not None:
+            def finish():
+                gslot.store.mark_ready(gslot.index)
+                bslot.store.mark_ready(bslot.index)
+            return gslot.grad, bslot.grad, finish
+        C = bn.num_features
+        dg = torch.empty((C,), device=bn.weight.device, dtype=torch.float32)
+        db = torch.empty((C,), device=bn.weight.device, dtype=torch.float32)
+
+        def finish_tmp():
+            _deliver_grad(bn.weight, lambda o: o.copy_(dg))
+            _deliver_grad(bn.bias, lambda o: o.copy_(db))
+        return dg, db, finish_tmp
+
     def _deliver_bn_grads(self, bn, run) -> None:
         """``run(dgamma_out, dbeta_out)`` writes dγ, dβ; route them into the flat store."""
         gslot = getattr(bn.weight, "_slot", None)
@@ -287,6 +343,8 @@ class FusedStages:
         independent work (a weight gradient) before ``_bn_bwd_finish``.  Single GPU: nothing
         to wait for (one fused launch in the finish)."""
         C = bn.num_features
+        if isinstance(partial, tuple) and partial[0] == "tail":
+            return ("done", bn, partial[1], None, bs)  # finalized by the dgrad's last blocks
         if not st.comm or st.ipc is not None:
             return ("local", bn, partial, nblk_seg, bs, st.ipc)
         dev = partial.device
@@ -301,6 +359,8 @@ class FusedStages:
     def _bn_bwd_finish(self, ops, h, S: int) -> torch.Tensor:
         """Phase 2: coef [3][S][C] for the input gradient (from the global sums)."""
         bn, bs = h[1], h[4]
+        if h[0] == "done":
+            return h[2]
         C = bn.num_features
         dev = bs.mi.device
         coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
@@ -365,7 +425,7 @@ class FusedStages:
 
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
                dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,
-               bnb: Optional[Tuple] = None):
+               bnb: Optional[Tuple] = None, tail_bn: Optional[Tuple] = None):
         """dx (NHWC) = conv-transpose(dy).  ``accumulate``: dx += result (dx must be given).
 
         ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
@@ -379,6 +439,9 @@ class FusedStages:
                                           the partials of its downsample BN too → (p3, pd)
         ``bnb = (a, coef)`` (1x1 stride-1 only): the A operand is the BatchNorm backward
         coef.A·dyn + coef.B·a + coef.D computed in the prologue.
+        ``tail_bn = (bn, bn_state, st)``: when the partials come from ONE launch (stride 1, no
+        second BN stream) its last blocks also finalize that BatchNorm's backward — the
+        partials entry of the result is then ("tail", coef) with dγ, dβ already delivered.
         """
         Nb, H, W, Ci = in_shape
         _, OH, OW, Co = dyn.shape
@@ -452,6 +515,18 @@ class FusedStages:
         if bn_epi[0] == "res" and bn_epi[5] is not None:
             partial2 = torch.empty_like(partial)
             second = (bn_epi[5], bn_epi[6], partial2)
+        if (tail_bn is not None and len(chosen) == 1 and second is None
+                and self._tail_ok(tail_bn[2], Ci, S)):
+            bn, bs, st = tail_bn
+            wt, g, M, seg, bm, v = chosen[0]
+            coef = torch.empty((3 * S * Ci,), device=dev, dtype=torch.float32)
+            dg, db, finish = self._bn_grad_targets(bn)
+            tail = self._tail_spec(bn, 2, S, st, 0, bs.count, bs.mi, dgamma=dg, dbeta=db,
+                                   coef=coef)
+            igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
+                         epi_tables=tables, bnb=bpro, tail=tail)
+            finish()
+            return dx, ("tail", coef), seg_blocks
         base = 0
         for wt, g, M, seg, bm, v in chosen:
             igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
@@ -565,15 +640,16 @@ class FusedStages:
                     cur, pro_ss = bmat, None
                 tp.ins.append((cur, pro_ss))
                 if ci_ == 0 and dual is not None:
-                    a, partial, nblk = self._conv_fwd(ops, cur, cs, None, S, dual=dual)
+                    a, partial, nblk, bs = self._conv_fwd(ops, cur, cs, None, S, dual=dual, st=st)
                     self.dual_launches += 1
                     if b.down is not None and br is not None:
                         fork_down()  # after the launch that writes its input x
                         forked = True
                 else:
-                    a, partial, nblk = self._conv_fwd(ops, cur, cs, pro_ss, S)
-                rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
-                bs = self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st)
+                    a, partial, nblk, bs = self._conv_fwd(ops, cur, cs, pro_ss, S, st=st)
+                if bs is None:
+                    rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
+                    bs = self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st)
                 tp.acts.append(a)
                 tp.bns.append(bs)
                 cur, pro_ss = a, bs.ss
@@ -613,10 +689,12 @@ class FusedStages:
         return self._branch
 
     def _down_fwd(self, ops, b: _BlockSpec, tp: _BlockTape, x, S: int, st, slot: int = 0):
-        ad, partial, nblk = self._conv_fwd(ops, x, b.down, None, S)
-        rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
+        ad, partial, nblk, bs = self._conv_fwd(ops, x, b.down, None, S, st=st, slot=slot)
         tp.ad = ad
-        tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st, slot=slot)
+        if bs is None:
+            rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
+            bs = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st, slot=slot)
+        tp.bnd = bs
 
     def backward(self, gout: torch.Tensor, tapes: List[_BlockTape]) -> torch.Tensor:
         ops = _ext.ops()
@@ -718,7 +796,8 @@ class FusedStages:
             _ext.TAG = f"{b.name} conv{i + 1} dgrad"
             dyn, bnb = (g3, lazy) if (i == L and lazy is not None) else (da, None)
             gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,
-                                       bn_epi=("mask", a_prev, bs_prev), bnb=bnb)
+                                       bn_epi=("mask", a_prev, bs_prev), bnb=bnb,
+                                       tail_bn=(b.convs[i - 1].bn, bs_prev, st))
             h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
             _ext.TAG = f"{b.name} conv{i + 1} wgrad"
             self._wgrad(ops, dyn, xin, cs, pro_ss, S, bnb=bnb)
@@ -748,7 +827,8 @@ class FusedStages:
                                        dx=resid if b.down is not None else None,
                                        bn_epi=("res", resid, ptp.mask, ptp.acts[-1],
                                                ptp.bns[-1].mi, ptp.ad if pds else None,
-                                               ptp.bnd.mi if pds else None))
+                                               ptp.bnd.mi if pds else None),
+                                       tail_bn=(pb.convs[-1].bn, ptp.bns[-1], st))
             if pds:
                 p3, pd = part
                 h = (self._bn_bwd_start(ops, pb.convs[-1].bn, p3, nb, ptp.bns[-1], S, st),

@@ -83,9 +83,11 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
                  seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None,
-                 bnb=None, dual=None) -> None:
+                 bnb=None, dual=None, tail=None) -> None:
     """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip);
     ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue;
+    ``tail = (mode, tensors, floats, ints)``: the BatchNorm that consumes ``stats`` is reduced and
+    finalized by this launch's last blocks (csrc/bn_tail.h; see FusedStages._tail_spec);
     ``dual = (res, rss, out, mask)``: block-output prologue — A is a block's pre-BN conv3
     activation, ``pro`` its BN scale/shift, ``res`` the residual (``rss`` its BN [2][S][C] table
     or None for identity); the conv consumes relu(bn(A) + res') and also writes it to ``out``
@@ -102,8 +104,13 @@ def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=N
     em = epi[4] if epi is not None and len(epi) > 4 else None
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     c2, mi2, st2 = second if second is not None else (None, None, None)
-    ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask)
+    if tail is None:
+        ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
+                  seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask)
+    else:  # ``tail = (mode, tensors, floats, ints)``: BatchNorm finalize in the last blocks
+        ops.igemm_t(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess,
+                    emi, seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout,
+                    pmask, tail[0], tail[1], tail[2], tail[3])
 
 
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):
