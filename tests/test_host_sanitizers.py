@@ -48,9 +48,8 @@ def test_host_code_clean_under_asan_ubsan():
             assert r.returncode == 0, r.stderr[-4000:]
         with cf.ThreadPoolExecutor(max_workers=6) as ex:
             list(ex.map(cc, zip(srcs, objs)))
-        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-fsanitize=address",
-                            "-fsanitize=undefined", *map(str, objs), "-o", str(exe)],
-                           capture_output=True, text=True)
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", *SAN[:4], *map(str, objs), "-o",
+                            str(exe)], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr[-4000:]
         for o in objs:
             o.unlink()
