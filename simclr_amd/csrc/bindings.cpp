@@ -112,6 +112,10 @@ void set_tail(ConvFusion& f, const ConvGeom& g, int64_t M, int bm, int bn, const
               int64_t stats_seg_blocks, int64_t epi_mode, const c10::optional<Tensor>& stats2,
               int64_t mode, const std::vector<c10::optional<Tensor>>& t,
               const std::vector<double>& tf, const std::vector<int64_t>& ti) {
+#ifndef SIMCLR_BN_TAIL
+  TORCH_CHECK(false, "igemm tail: this build has no conv-tail BatchNorm finalize (rebuild with "
+                     "SIMCLR_BUILD_BN_TAIL=1)");
+#endif
   TORCH_CHECK(mode == 1 || mode == 2, "igemm tail: mode 1 (forward) or 2 (backward)");
   TORCH_CHECK(stats.defined() && stats.numel() > 0 && f.seg_rows > 0 && stats_seg_blocks == 0,
               "igemm tail: needs the stats partials of one launch with seg_rows");

@@ -143,9 +143,10 @@ class FusedStages:
         self.block_out_min_hw = int(v) if v.isdigit() else 1
         self.block_out_prologue = self.block_out_min_hw > 0
         # BatchNorm reduce + finalize in the producing conv kernel's last blocks (csrc/bn_tail.h)
-        # instead of a separate reduce launch per BatchNorm.  Off by default: every block then
-        # has to drain its stores (incl. the nontemporal output tile) before its ticket, which
-        # costs more than the launches it saves (24.33 -> 25.59 ms/step A/B, r2 log)
+        # instead of a separate reduce launch per BatchNorm.  Off by default and compiled only
+        # by SIMCLR_BUILD_BN_TAIL=1 builds: every block has to drain its stores (incl. the
+        # nontemporal output tile) before its ticket, which costs more than the launches it
+        # saves (24.33 -> 25.59 ms/step A/B, r2 log)
         self.bn_tail = os.environ.get("SIMCLR_BN_TAIL", "0") == "1"
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
