@@ -196,7 +196,7 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const c10::optional<Tensor>& pro_rss, const c10::optional<Tensor>& pro_out,
            const c10::optional<Tensor>& pro_mask, int64_t tail_mode,
            const std::vector<c10::optional<Tensor>>& tail_t, std::vector<double> tail_f,
-           std::vector<int64_t> tail_i) {
+           std::vector<int64_t> tail_i, int64_t stats_groups) {
   const ConvGeom g = geom_from(gv);
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
@@ -221,7 +221,7 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   }
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
   const bool has_stats = stats.has_value() && stats->defined();
-  if (has_stats && stats_seg_blocks == 0)
+  if (has_stats && stats_seg_blocks == 0 && stats_groups == 0)
     TORCH_CHECK(stats->numel() >= ((M + bm - 1) / bm) * 2 * g.N, "igemm: stats buffer too small");
   ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, 1, epi_mode, epi_a, epi_b,
                              g.C, out.numel());
@@ -236,7 +236,7 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
     const int64_t nseg = M / seg_rows;
     TORCH_CHECK(stats_base >= 0 && stats_base + seg_rows / bm <= stats_seg_blocks,
                 "igemm: stats remap window out of range");
-    TORCH_CHECK(stats->numel() >= nseg * stats_seg_blocks * 2 * g.N,
+    TORCH_CHECK(stats_groups > 0 || stats->numel() >= nseg * stats_seg_blocks * 2 * g.N,
                 "igemm: remapped stats buffer too small");
   }
   if (epi_mode == 3 || epi_mode == 4) {
@@ -314,6 +314,15 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
       f.pro_rsh = f.pro_rsc + nseg * g.C;
     }
   }
+  if (stats_groups > 0) {
+    TORCH_CHECK(has_stats && seg_rows > 0 && tail_mode == 0 && stats_groups <= 64,
+                "igemm: atomic stats replicas need stats, seg_rows, no tail, <= 64 groups");
+    TORCH_CHECK(stats->numel() >= (M / seg_rows) * stats_groups * 2 * g.N,
+                "igemm: atomic stats buffer too small ([S][G][2][N])");
+    if (stats2.has_value() && stats2->defined())
+      TORCH_CHECK(stats2->numel() >= stats->numel(), "igemm: stats2 buffer too small");
+    f.stats_groups = (int)stats_groups;
+  }
   if (tail_mode != 0) set_tail(f, g, M, bm, igemm_variant_bn((int)variant), has_stats ? *stats : out, stats_seg_blocks, epi_mode,
                                stats2, tail_mode, tail_t, tail_f, tail_i);
   conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
@@ -332,10 +341,33 @@ void igemm_plain(const Tensor& A, const Tensor& B, const Tensor& out,
                  const c10::optional<Tensor>& epi_c2, const c10::optional<Tensor>& epi_mi2,
                  const c10::optional<Tensor>& stats2, const c10::optional<Tensor>& pro_d,
                  const c10::optional<Tensor>& A2, const c10::optional<Tensor>& pro_rss,
-                 const c10::optional<Tensor>& pro_out, const c10::optional<Tensor>& pro_mask) {
+                 const c10::optional<Tensor>& pro_out, const c10::optional<Tensor>& pro_mask,
+                 int64_t stats_groups) {
   igemm(A, B, out, bias, stats, std::move(gv), pro_sc, pro_sh, pro_seg_rows, pro_relu, epi_mode,
         epi_a, epi_b, variant, epi_ss, epi_mi, seg_rows, stats_seg_blocks, stats_base, epi_c,
-        epi_mask, epi_c2, epi_mi2, stats2, pro_d, A2, pro_rss, pro_out, pro_mask, 0, {}, {}, {});
+        epi_mask, epi_c2, epi_mi2, stats2, pro_d, A2, pro_rss, pro_out, pro_mask, 0, {}, {}, {},
+        stats_groups);
+}
+
+void igemm_tailed(const Tensor& A, const Tensor& B, const Tensor& out,
+                  const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
+                  std::vector<int64_t> gv, const c10::optional<Tensor>& pro_sc,
+                  const c10::optional<Tensor>& pro_sh, int64_t pro_seg_rows, bool pro_relu,
+                  int64_t epi_mode, const c10::optional<Tensor>& epi_a,
+                  const c10::optional<Tensor>& epi_b, int64_t variant,
+                  const c10::optional<Tensor>& epi_ss, const c10::optional<Tensor>& epi_mi,
+                  int64_t seg_rows, int64_t stats_seg_blocks, int64_t stats_base,
+                  const c10::optional<Tensor>& epi_c, const c10::optional<Tensor>& epi_mask,
+                  const c10::optional<Tensor>& epi_c2, const c10::optional<Tensor>& epi_mi2,
+                  const c10::optional<Tensor>& stats2, const c10::optional<Tensor>& pro_d,
+                  const c10::optional<Tensor>& A2, const c10::optional<Tensor>& pro_rss,
+                  const c10::optional<Tensor>& pro_out, const c10::optional<Tensor>& pro_mask,
+                  int64_t tail_mode, const std::vector<c10::optional<Tensor>>& tail_t,
+                  std::vector<double> tail_f, std::vector<int64_t> tail_i) {
+  igemm(A, B, out, bias, stats, std::move(gv), pro_sc, pro_sh, pro_seg_rows, pro_relu, epi_mode,
+        epi_a, epi_b, variant, epi_ss, epi_mi, seg_rows, stats_seg_blocks, stats_base, epi_c,
+        epi_mask, epi_c2, epi_mi2, stats2, pro_d, A2, pro_rss, pro_out, pro_mask, tail_mode,
+        tail_t, std::move(tail_f), std::move(tail_i), 0);
 }
 
 int64_t igemm_bm(int64_t N) { return igemm_block_m((int)N); }
@@ -545,8 +577,11 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
                         const c10::optional<Tensor>& ipc_peers,
                         const c10::optional<Tensor>& ipc_arena, int64_t ipc_site,
                         const c10::optional<Tensor>& ipc_epoch,
-                        const c10::optional<Tensor>& ipc_err, int64_t world, int64_t rank) {
+                        const c10::optional<Tensor>& ipc_err, int64_t world, int64_t rank,
+                        bool zero_after) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "bn_reduce_fused: mode");
+  TORCH_CHECK(!zero_after || nblk <= bn_reduce_direct_rows(),
+              "bn_reduce_fused: zero_after needs the one-pass (direct) reduction");
   TORCH_CHECK(nblk > 0 && partial.numel() >= S * nblk * 2 * C, "bn_reduce_fused: partial size");
   TORCH_CHECK(C % 4 == 0, "bn_reduce_fused: C must be a multiple of 4 (float4 partial rows)");
   TORCH_CHECK(S >= 1 && S <= 4, "bn_reduce_fused: at most 4 segments");
@@ -557,6 +592,7 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
   at::Tensor ws = at::empty({S * G * 2 * C}, partial.options());
   q.ws = ws.data_ptr<float>();
   q.tickets = tickets_for(partial, (C + 63) / 64, ticket_slot);
+  q.zero_after = zero_after ? 1 : 0;
   q.count = (float)count; q.eps = (float)eps; q.momentum = (float)momentum;
   if (mode == 0) {
     TORCH_CHECK(stats.has_value() && stats->numel() >= 2 * S * C, "bn_reduce_fused: stats");
@@ -908,8 +944,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
   m.def("ce_topk(Tensor logits, Tensor y, float gscale, Tensor(a!) loss, Tensor(b!) rank, Tensor(c!)? dlogits=None) -> ()", &ce_topk_op);
   m.def("class_sums(Tensor X, Tensor y, int NC, Tensor(a!) sums, Tensor(b!) counts) -> ()", &class_sums_op);
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm_plain);
-  m.def("igemm_t(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc, Tensor? pro_sh, int pro_seg_rows, bool pro_relu, int epi_mode, Tensor? epi_a, Tensor? epi_b, int variant, Tensor? epi_ss, Tensor? epi_mi, int seg_rows, int stats_seg_blocks, int stats_base, Tensor? epi_c, Tensor? epi_mask, Tensor? epi_c2, Tensor? epi_mi2, Tensor(c!)? stats2, Tensor? pro_d, Tensor? A2, Tensor? pro_rss, Tensor(d!)? pro_out, Tensor(e!)? pro_mask, int tail_mode, Tensor(f!)?[] tail_t, float[] tail_f, int[] tail_i) -> ()", &igemm);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None, int stats_groups=0) -> ()", &igemm_plain);
+  m.def("igemm_t(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc, Tensor? pro_sh, int pro_seg_rows, bool pro_relu, int epi_mode, Tensor? epi_a, Tensor? epi_b, int variant, Tensor? epi_ss, Tensor? epi_mi, int seg_rows, int stats_seg_blocks, int stats_base, Tensor? epi_c, Tensor? epi_mask, Tensor? epi_c2, Tensor? epi_mi2, Tensor(c!)? stats2, Tensor? pro_d, Tensor? A2, Tensor? pro_rss, Tensor(d!)? pro_out, Tensor(e!)? pro_mask, int tail_mode, Tensor(f!)?[] tail_t, float[] tail_f, int[] tail_i) -> ()", &igemm_tailed);
   m.def("igemm_dual_ok(int v, int[] geom) -> bool", &igemm_dok);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
@@ -930,7 +966,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
   m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
-  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0) -> ()", &bn_reduce_fused_op);
+  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0, bool zero_after=False) -> ()", &bn_reduce_fused_op);
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);

@@ -178,6 +178,7 @@ struct BnReduceArgs {
   unsigned* epoch;
   int* err;
   int world, rank;
+  int zero_after;
 };
 
 constexpr int kMaxSeg = 4;  // BatchNorm segments (views) per launch handled by the reducer
@@ -345,8 +346,12 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
 #pragma unroll
         for (int sg = 0; sg < kMaxSeg; ++sg) {
           if (sg < S) {
-            const float4 v = *(const float4*)(base + (((size_t)sg * G + g) * 2) * C);
+            float4* src = (float4*)(base + (((size_t)sg * G + g) * 2) * C);
+            const float4 v = *src;
             acc[sg].x += v.x; acc[sg].y += v.y; acc[sg].z += v.z; acc[sg].w += v.w;
+            // atomic accumulators (conv stats_groups) are ready for the next step once read:
+            // each element has exactly one reader (direct mode)
+            if (p.zero_after) *src = make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
       }
@@ -981,6 +986,7 @@ void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s) {
   a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.coef = q.coef;
   a.peers = q.ipc_peers; a.own = q.ipc_own; a.site = q.ipc_site; a.epoch = q.ipc_epoch;
   a.err = q.ipc_err; a.world = q.world; a.rank = q.rank;
+  a.zero_after = q.zero_after;
   const dim3 grid = a.direct ? dim3((q.C + 63) / 64) : dim3((q.C + 63) / 64, q.S, a.G);
   if (a.world > 1 && a.peers != nullptr)
     hipLaunchKernelGGL(k_bn_reduce_fused<true>, grid, dim3(256), 0, s, a);

@@ -82,6 +82,10 @@ struct IgemmArgs {
   int seg_rows, stats_seg_blocks, stats_base;
   // BatchNorm finalize in this launch's last blocks (igemm_bn_tail; on == 0: partials only)
   BnTailArgs tail;
+  // > 0: the partials are accumulated with float atomics into stats_groups replica rows per
+  // segment ([S][G][2][N], zeroed by the reduce that consumes them) instead of one row per
+  // row-block: the reduce reads S·G rows in one pass (bn.hip direct mode)
+  int stats_groups;
 };
 
 __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const float* sh, bool ok,
@@ -455,7 +459,18 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
       const int blk = p.stats_seg_blocks > 0
                           ? seg * p.stats_seg_blocks + p.stats_base + (m0 - seg * p.seg_rows) / BM
                           : mb;
-      if (p.tail.on) {
+      if (p.stats_groups > 0) {
+        // replica g of this row-block's segment: 2048 row-blocks of a layer1 conv become
+        // 16 rows with ~128 uncontended adds per address, spread over L2 channels
+        const int segb = (p.stats_seg_blocks > 0 ? p.stats_base : 0) + (m0 - seg * p.seg_rows) / BM;
+        const size_t row = (size_t)seg * p.stats_groups + (segb % p.stats_groups);
+        unsafeAtomicAdd(&p.stats[(row * 2 + 0) * p.N + n0 + tid], a);
+        unsafeAtomicAdd(&p.stats[(row * 2 + 1) * p.N + n0 + tid], b);
+        if (two) {
+          unsafeAtomicAdd(&p.stats2[(row * 2 + 0) * p.N + n0 + tid], a);
+          unsafeAtomicAdd(&p.stats2[(row * 2 + 1) * p.N + n0 + tid], d);
+        }
+      } else if (p.tail.on) {
         // write-through (agent-scope) stores: this kernel's tail may read them from another
         // XCD (bn_tail.h); a separate reduce kernel sees plain stores at the kernel boundary
         __hip_atomic_store(&p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid], a, __ATOMIC_RELAXED,
@@ -466,7 +481,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
         p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
         p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
       }
-      if (two) {
+      if (two && p.stats_groups == 0) {
         p.stats2[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
         p.stats2[((size_t)blk * 2 + 1) * p.N + n0 + tid] = d;
       }
@@ -1985,6 +2000,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   a.tail = f.tail;
+  a.stats_groups = f.stats_groups;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
   if (a.pro_out != nullptr
           ? !igemm_dual_ok(variant, g)

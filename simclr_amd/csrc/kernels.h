@@ -84,6 +84,7 @@ struct ConvFusion {
   int stats_seg_blocks = 0;       // >0: segment-major stats rows (see conv.hip)
   int stats_base = 0;
   BnTailArgs tail;                // BatchNorm finalize in the kernel's last blocks (bn_tail.h)
+  int stats_groups = 0;           // >0: atomic partials in [S][G][2][N] replica rows (conv.hip)
 };
 int igemm_tail_ticket_words(int nNb, int S, int ngrp);
 void igemm_tail_plan(int nmb_seg, int* gr, int* ngrp);
@@ -153,6 +154,7 @@ struct BnReduceFusedParams {
   float* dgamma = nullptr;
   float* dbeta = nullptr;
   float* coef = nullptr;
+  int zero_after = 0;  // direct mode: zero the partial rows once read (atomic accumulators)
   // cross-rank exchange over IPC-mapped peer arenas (modes 1 / 2 at world > 1, see bn.hip)
   uint64_t* const* ipc_peers = nullptr;  // device array [world] of arena bases (own included)
   uint64_t* ipc_own = nullptr;           // this rank's arena base

@@ -148,6 +148,15 @@ class FusedStages:
         # nontemporal output tile) before its ticket, which costs more than the launches it
         # saves (24.33 -> 25.59 ms/step A/B, r2 log)
         self.bn_tail = os.environ.get("SIMCLR_BN_TAIL", "0") == "1"
+        # SIMCLR_STATS_GROUPS=G: conv-epilogue BatchNorm partials accumulated with float atomics
+        # into G replica rows per segment (persistent per-BatchNorm buffers, zeroed by the
+        # reduce that reads them), so the reduce is one pass over S·G rows instead of a sliced
+        # two-level pass over one row per row-block.  Off by default: measured neutral (24.10 vs
+        # 24.07 ms/step — the reduce launch's cost is its dispatch, not its reads) and atomic
+        # order is not reproducible; deterministic runs never use it.
+        g = os.environ.get("SIMCLR_STATS_GROUPS", "0")
+        self.stats_groups = int(g) if g.isdigit() else 0
+        self._accs = {}
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -195,6 +204,23 @@ class FusedStages:
         return True
 
     # ------------------------------------------------------------------ building blocks
+    def _groups(self) -> int:
+        """Replica rows per segment for atomic BatchNorm partials (0: one row per row-block)."""
+        if self.stats_groups <= 0 or torch.are_deterministic_algorithms_enabled():
+            return 0
+        return min(self.stats_groups, 64)
+
+    def _acc(self, key, S: int, G: int, C: int, dev) -> torch.Tensor:
+        """Persistent zeroed [S][G][2][C] accumulator of one BatchNorm site (the reduce that
+        reads it zeroes it again).  Allocated on first use — the eager warm-up steps, before any
+        hipGraph capture."""
+        n = S * G * 2 * C
+        t = self._accs.get(key)
+        if t is None or t.numel() != n or t.device != dev:
+            t = torch.zeros((n,), device=dev, dtype=torch.float32)
+            self._accs[key] = t
+        return t
+
     def _tail_ok(self, st, C: int, S: int) -> bool:
         return (getattr(self, "bn_tail", False) and C % 64 == 0 and S <= 2
                 and (not st.comm or st.ipc is not None))
@@ -242,6 +268,13 @@ class FusedStages:
             pro = (pro_ss[0], pro_ss[1], M // S, True)
         v = igemm_choose(ops, A, w, a, g, want_stats=True, pro=pro, seg_rows=M // S, dual=dl)
         bm = ops.igemm_variant_bm(v)
+        G = self._groups()
+        use_tail = st is not None and self._tail_ok(st, Co, S)
+        if G and not use_tail:  # atomic replica partials (see __init__)
+            stats = self._acc((id(cs.bn), "fwd"), S, G, Co, xn.device)
+            igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl, seg_rows=M // S,
+                         stats_groups=G)
+            return a, stats, -G, None  # negative: accumulator rows (reduce with zero_after)
         stats = torch.empty(((M // bm) * 2 * Co,), device=xn.device, dtype=torch.float32)
         tail, bs = None, None
         if st is not None and self._tail_ok(st, Co, S):
@@ -283,16 +316,20 @@ class FusedStages:
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ss = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ipc = st.ipc
+        zero = nblk_seg < 0  # atomic accumulator rows: read once, zeroed by the reduce
+        nblk_seg = abs(nblk_seg)
         if not st.comm or ipc is not None:
             # one launch: reduce + finalize (last-arriver); at world > 1 the IPC statistics
             # exchange runs inside it (comm/ipc.py)
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
                                 bn.weight.detach(), bn.bias.detach(), ss, None, None, None, slot,
-                                **(ipc.kwargs((id(bn), "fwd"), S, C) if ipc is not None else {}))
+                                **(ipc.kwargs((id(bn), "fwd"), S, C) if ipc is not None else {}),
+                                zero_after=zero)
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats, ticket_slot=slot)
+            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats, ticket_slot=slot,
+                                zero_after=zero)
             _allreduce(stats, st, branch=slot == 1)
             ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean,
                             bn.running_var, mi, bn.num_batches_tracked, bn.weight.detach(),
@@ -350,7 +387,7 @@ class FusedStages:
             return ("local", bn, partial, nblk_seg, bs, st.ipc)
         dev = partial.device
         sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, sums)
+        ops.bn_reduce_fused(partial, abs(nblk_seg), S, C, 0, sums, zero_after=nblk_seg < 0)
         scratch = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
         self._deliver_bn_grads(bn, lambda dg, db: ops.bn_bwd_finalize(
             sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db, scratch))
@@ -371,8 +408,9 @@ class FusedStages:
             partial, nblk_seg, ipc = h[2], h[3], h[5]
             kw = ipc.kwargs((id(bn), "bwd"), S, C) if ipc is not None else {}
             self._deliver_bn_grads(bn, lambda dg, db: ops.bn_reduce_fused(
-                partial, nblk_seg, S, C, 2, None, bs.count, 0.0, 0.0, None, None, bs.mi, None,
-                bn.weight.detach(), None, None, dg, db, coef, **kw))
+                partial, abs(nblk_seg), S, C, 2, None, bs.count, 0.0, 0.0, None, None, bs.mi,
+                None, bn.weight.detach(), None, None, dg, db, coef, **kw,
+                zero_after=nblk_seg < 0))
         else:
             sums, work = h[2], h[3]
             work.wait()
@@ -426,7 +464,8 @@ class FusedStages:
 
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
                dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,
-               bnb: Optional[Tuple] = None, tail_bn: Optional[Tuple] = None):
+               bnb: Optional[Tuple] = None, tail_bn: Optional[Tuple] = None,
+               acc_keys: Optional[Tuple] = None):
         """dx (NHWC) = conv-transpose(dy).  ``accumulate``: dx += result (dx must be given).
 
         ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
@@ -440,6 +479,8 @@ class FusedStages:
                                           the partials of its downsample BN too → (p3, pd)
         ``bnb = (a, coef)`` (1x1 stride-1 only): the A operand is the BatchNorm backward
         coef.A·dyn + coef.B·a + coef.D computed in the prologue.
+        ``acc_keys = (key, key2)``: BatchNorm sites of the partials (and of the second stream)
+        for the atomic accumulators; blocks-per-segment is then returned negative (-G).
         ``tail_bn = (bn, bn_state, st)``: when the partials come from ONE launch (stride 1, no
         second BN stream) its last blocks also finalize that BatchNorm's backward — the
         partials entry of the result is then ("tail", coef) with dγ, dβ already delivered.
@@ -511,6 +552,24 @@ class FusedStages:
                              epi_tables=tables, bnb=bpro)
             chosen.append((wt, g, M, seg, ops.igemm_variant_bm(v), v))
         seg_blocks = sum(seg // bm for (_, _, _, seg, bm, _) in chosen)
+        G = self._groups() if acc_keys is not None else 0
+        use_tail = (tail_bn is not None and len(chosen) == 1 and self._tail_ok(tail_bn[2], Ci, S)
+                    and not (bn_epi[0] == "res" and bn_epi[5] is not None))
+        if G and not use_tail:  # atomic replica partials (see __init__)
+            partial = self._acc(acc_keys[0], S, G, Ci, dev)
+            second, partial2 = None, None
+            if bn_epi[0] == "res" and bn_epi[5] is not None:
+                partial2 = self._acc(acc_keys[1], S, G, Ci, dev)
+                second = (bn_epi[5], bn_epi[6], partial2)
+            base = 0
+            for wt, g, M, seg, bm, v in chosen:
+                igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
+                             epi_tables=tables, remap=(seg_blocks, base), second=second,
+                             bnb=bpro, stats_groups=G)
+                base += seg // bm
+            if partial2 is not None:
+                return dx, (partial, partial2), -G
+            return dx, partial, -G
         partial = torch.empty((S * seg_blocks * 2 * Ci,), device=dev, dtype=torch.float32)
         second, partial2 = None, None
         if bn_epi[0] == "res" and bn_epi[5] is not None:
@@ -798,7 +857,8 @@ class FusedStages:
             dyn, bnb = (g3, lazy) if (i == L and lazy is not None) else (da, None)
             gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,
                                        bn_epi=("mask", a_prev, bs_prev), bnb=bnb,
-                                       tail_bn=(b.convs[i - 1].bn, bs_prev, st))
+                                       tail_bn=(b.convs[i - 1].bn, bs_prev, st),
+                                       acc_keys=((id(b.convs[i - 1].bn), "bwd"), None))
             h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
             _ext.TAG = f"{b.name} conv{i + 1} wgrad"
             self._wgrad(ops, dyn, xin, cs, pro_ss, S, bnb=bnb)
@@ -829,7 +889,9 @@ class FusedStages:
                                        bn_epi=("res", resid, ptp.mask, ptp.acts[-1],
                                                ptp.bns[-1].mi, ptp.ad if pds else None,
                                                ptp.bnd.mi if pds else None),
-                                       tail_bn=(pb.convs[-1].bn, ptp.bns[-1], st))
+                                       tail_bn=(pb.convs[-1].bn, ptp.bns[-1], st),
+                                       acc_keys=((id(pb.convs[-1].bn), "bwd"),
+                                                 (id(pb.down.bn), "bwd") if pds else None))
             if pds:
                 p3, pd = part
                 h = (self._bn_bwd_start(ops, pb.convs[-1].bn, p3, nb, ptp.bns[-1], S, st),

@@ -83,9 +83,11 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
                  seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None,
-                 bnb=None, dual=None, tail=None) -> None:
+                 bnb=None, dual=None, tail=None, stats_groups: int = 0) -> None:
     """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip);
     ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue;
+    ``stats_groups = G > 0``: ``stats`` is a zeroed [S][G][2][N] accumulator the epilogue adds
+    its partials into with float atomics (replica = row-block index mod G, conv.hip);
     ``tail = (mode, tensors, floats, ints)``: the BatchNorm that consumes ``stats`` is reduced and
     finalized by this launch's last blocks (csrc/bn_tail.h; see FusedStages._tail_spec);
     ``dual = (res, rss, out, mask)``: block-output prologue — A is a block's pre-BN conv3
@@ -106,7 +108,8 @@ def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=N
     c2, mi2, st2 = second if second is not None else (None, None, None)
     if tail is None:
         ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-                  seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask)
+                  seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask,
+                  stats_groups)
     else:  # ``tail = (mode, tensors, floats, ints)``: BatchNorm finalize in the last blocks
         ops.igemm_t(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess,
                     emi, seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout,
