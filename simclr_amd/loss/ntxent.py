@@ -150,13 +150,16 @@ class _NTXentHipFn(torch.autograd.Function):
 
 class NTXent(nn.Module):
     def __init__(self, temperature: float = 0.1, reduction: str = "mean",
-                 device: Optional[torch.device] = None, gather: bool = False):
+                 device: Optional[torch.device] = None, gather=False):
+        """``gather``: False (reference, per-GPU negatives), True (all-gathered global
+        negatives, fused kernel) or ``"ring"`` (global negatives circulated around the ranks,
+        loss/ring.py)."""
         assert temperature > 0.0
         assert reduction in {"none", "mean", "sum"}
         super().__init__()
         self.temperature = temperature
         self.reduction = reduction
-        self.gather = gather
+        self.gather = "ring" if str(gather).lower() == "ring" else bool(gather)
 
     def forward(self, view0: torch.Tensor, view1: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``forward(view0, view1)`` as the reference, or ``forward(z)`` with z = [view0; view1]."""
@@ -168,6 +171,12 @@ class NTXent(nn.Module):
             n = z.shape[0] // 2
         st = pstate.get()
         R, D = z.shape
+        if self.gather == "ring" and st.comm and st.world_size > 1:
+            # global negatives with the column blocks circulating around the ranks (loss/ring.py)
+            from .ring import nt_xent_ring
+            if self.reduction != "mean":
+                raise ValueError("ring NT-Xent supports reduction='mean'")
+            return nt_xent_ring(z, n, self.temperature, st.group, st.world_size, st.rank)
         if (z.is_cuda and self.reduction != "none" and registry.use_hip(z) and R % 16 == 0
                 and D in (32, 64, 128, 256)):
             return _NTXentHipFn.apply(z, n, self.temperature, self.reduction, self.gather, st)

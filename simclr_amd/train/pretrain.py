@@ -78,7 +78,7 @@ class Trainer:
                              schedule_mode=MODE_WARMUP_COSINE, warmup_steps=self.warmup_steps,
                              total_steps=self.total_steps)
         self.loss_fn = NTXent(temperature=cfg["parameter"]["temperature"],
-                              gather=bool(cfg_get(cfg, "loss.gather", False)))
+                              gather=cfg_get(cfg, "loss.gather", False))
         self.hip = self.device.type == "cuda" and registry.use_hip(self.store.master) \
             and self.precision == "bf16"
         self.model.train()
