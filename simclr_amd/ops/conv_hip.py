@@ -40,6 +40,11 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
         A2, rss, pout, pmask = dual
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ess, emi = epi_tables if epi_tables is not None else (None, None)
+    key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows,
+           bnb is not None, dual is not None)
+    hit = tuning.cached(key)
+    if hit is not None:  # steady state: no per-launch walk over the variant table
+        return hit
     cands = []
     for v in range(ops.igemm_nvariants()):
         bm = ops.igemm_variant_bm(v)
@@ -61,8 +66,6 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
     default = 1 if N <= 64 else 0
     if default not in cands:
         default = cands[0]
-    key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows,
-           bnb is not None, dual is not None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
     em = epi[4] if epi is not None and len(epi) > 4 else None
 
@@ -166,10 +169,12 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
         ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v,
                   dY2, dcoef, dseg, dS)
 
-    cands = [v for v in range(ops.wgrad_nvariants())
-             if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)]
-    v = tuning.pick(key, cands, 1 if N <= 64 else 0,
-                    lambda vv: launch(vv, torch.empty_like(out)))
+    v = tuning.cached(key)
+    if v is None:
+        cands = [v for v in range(ops.wgrad_nvariants())
+                 if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)]
+        v = tuning.pick(key, cands, 1 if N <= 64 else 0,
+                        lambda vv: launch(vv, torch.empty_like(out)))
     launch(v, out)
 
 

@@ -20,6 +20,8 @@ def set_enabled(on: bool) -> None:
     """``runtime.deterministic`` turns tuning off: timing-driven choices differ run to run, and
     with them the fp32 summation order of a kernel (bitwise reproducibility needs fixed tiles)."""
     global ENABLED
+    if bool(on) != ENABLED:
+        _CACHE.clear()  # choices made under the other policy (timed vs fixed) must not leak
     ENABLED = bool(on)
 
 
@@ -36,7 +38,10 @@ def pick(key: Hashable, candidates: Sequence[int], default: int,
         return default
     if (not ENABLED or len(cands) == 1 or not torch.cuda.is_available()
             or torch.cuda.is_current_stream_capturing()):
-        return default if default in cands else cands[0]
+        choice = default if default in cands else cands[0]
+        if not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+            _CACHE[key] = choice  # fixed choice: later launches skip the candidate walk
+        return choice
     best, best_t = cands[0], float("inf")
     for v in cands:
         run(v)
