@@ -107,6 +107,19 @@ def run_ours(args, rank, world, dev):
             it = iter(loader)
             return next(it)[0]
 
+    def timed(k):
+        _sync(dev, world)
+        t = time.perf_counter()
+        for _ in range(k):
+            tr.step(next_batch())
+        _sync(dev, world)
+        return time.perf_counter() - t
+
+    auto = args.graph == "auto"
+    t_eager = None
+    if auto and tr.hip:
+        timed(2)  # eager warm-up: autotuning, allocator, communicators
+        t_eager = timed(3)
     if args.graph and tr.hip:
         try:
             tr.capture(next_batch())
@@ -115,6 +128,18 @@ def run_ours(args, rank, world, dev):
                   file=sys.stderr, flush=True)
             tr.graph = None
             args.graph = False
+    if auto and tr.graph is not None and t_eager is not None:
+        # execution-mode autotune: replaying the captured step vs issuing it eagerly (the HIP
+        # graph executor loses part of the side-stream overlap — 24.0 vs 23.4 ms/step at N=1 —
+        # while eager issue costs host time that grows with the ranks sharing the CPUs)
+        t_graph = timed(3)
+        tt = torch.tensor([t_eager, t_graph], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        if float(tt[1]) >= float(tt[0]):
+            tr.graph = None
+        args.mode_probe_ms = [round(float(v) / 3 * 1000.0, 3) for v in tt.tolist()]
+    args.graph = tr.graph is not None
     loss = None
     import contextlib
     ctx = contextlib.nullcontext()
@@ -212,8 +237,9 @@ def main(argv=None):
     ap.add_argument("--local-loss", dest="gather", action="store_false",
                     help="per-GPU NT-Xent, the reference's loss (loss.py has no collective)")
     ap.add_argument("--graph", action="store_true", default=None,
-                    help="capture the step in a hipGraph (default: on)")
-    ap.add_argument("--no-graph", dest="graph", action="store_false")
+                    help="capture the step in a hipGraph and replay it")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="issue every step eagerly (default: probe both, keep the faster)")
     ap.add_argument("--bucket-mb", dest="bucket_mb", type=float, default=32.0)
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     args = ap.parse_args(argv)
@@ -221,11 +247,12 @@ def main(argv=None):
     if args.gather is None:
         args.gather = world > 1
     if args.graph is None:
-        # the whole step, RCCL collectives included (thread-local capture mode), is one hipGraph
-        # at every N: replays issue no per-kernel host work, so 8 ranks sharing the host CPUs
-        # cannot become launch-bound
-        # (gloo rehearsals on one GPU stay eager: host collectives cannot be captured)
-        args.graph = not dist.is_initialized() or dist.get_backend() == "nccl"
+        # default: probe the eager step and the hipGraph replay of the whole step (RCCL
+        # collectives included, thread-local capture mode) for 3 steps each and keep the faster
+        # (same decision on every rank); gloo rehearsals on one GPU stay eager (host collectives
+        # cannot be captured)
+        args.graph = "auto" if (not dist.is_initialized() or dist.get_backend() == "nccl") \
+            else False
     args.bn_comm = "none"
     if args.impl == "ours":
         dt, loss = run_ours(args, rank, world, dev)
@@ -278,6 +305,7 @@ def main(argv=None):
             "optimizer": "LARS(trust=1e-3)+SGD(m=0.9), warmup+cosine",
             "impl": args.impl,
             "hip_graph": bool(args.graph and args.impl == "ours"),
+            "exec_mode_probe_ms_eager_graph": getattr(args, "mode_probe_ms", None),
             "bn_stats_comm": args.bn_comm,
             "host_issue_ms_per_step": (round(args.host_issue_ms, 3)
                                        if hasattr(args, "host_issue_ms") else None),
