@@ -134,8 +134,9 @@ __global__ __launch_bounds__(256) void k_ce_topk(const float* __restrict__ logit
   }
   const float lse = m + __logf(s);
   if (lane == 0) {
-    loss[row] = lse - zt;
-    rank[row] = above;
+    const bool valid = t >= 0 && t < C;
+    loss[row] = lse - zt;             // NaN for an out-of-range label (as F.cross_entropy errors)
+    rank[row] = valid ? above : C;    // never counted as correct
   }
   if (dlogits != nullptr) {
     float* d = dlogits + (size_t)row * C;
