@@ -30,7 +30,7 @@ from ..parallel import state as pstate
 def nt_xent_torch(z: torch.Tensor, n: int, temperature: float, reduction: str = "mean",
                   gather: bool = False, group=None, world_size: int = 1, rank: int = 0):
     """Oracle implementation on torch ops; ``z`` = [view0; view1] of shape [2n, d]."""
-    zn = F.normalize(z.float(), p=2, dim=1)
+    zn = F.normalize(z if z.dtype == torch.float64 else z.float(), p=2, dim=1)
     R = zn.shape[0]
     if gather and world_size > 1:
         from torch.distributed.nn.functional import all_gather

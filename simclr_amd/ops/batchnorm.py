@@ -29,6 +29,13 @@ from torch import nn
 from . import registry
 
 
+def _acc(t: torch.Tensor) -> torch.Tensor:
+    """Accumulation precision of the torch oracles: fp32, or fp64 when the input is fp64 (the
+    multi-process equivalence tests run in fp64 so that summation-order noise cannot hide a
+    semantic difference)."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
 class _BatchNormBase(nn.Module):
     def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1):
         super().__init__()
@@ -74,7 +81,7 @@ def reference_batch_norm_train(x: torch.Tensor, bn: _BatchNormBase, segments: in
     n = N // segments
     chan_last = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) \
         and not x.is_contiguous()
-    xf = x.float().reshape(segments, n, C, -1)
+    xf = _acc(x).reshape(segments, n, C, -1)
     L = xf.shape[-1]
     s1 = xf.sum(dim=(1, 3))
     s2 = (xf * xf).sum(dim=(1, 3))
@@ -87,12 +94,12 @@ def reference_batch_norm_train(x: torch.Tensor, bn: _BatchNormBase, segments: in
     mean = stats[0] / count
     var = (stats[1] / count - mean * mean).clamp_min(0.0)
     invstd = torch.rsqrt(var + bn.eps)
-    w = bn.weight.float()
-    b = bn.bias.float()
+    w = _acc(bn.weight)
+    b = _acc(bn.bias)
     y = (xf - mean[:, None, :, None]) * (invstd * w)[:, None, :, None] + b[None, None, :, None]
     y = y.reshape(x.shape)
     if residual is not None:
-        y = y + residual.float()
+        y = y + _acc(residual)
     if relu:
         y = torch.relu(y)
     with torch.no_grad():
@@ -112,12 +119,12 @@ def reference_batch_norm_eval(x: torch.Tensor, bn: _BatchNormBase,
                               residual: Optional[torch.Tensor], relu: bool) -> torch.Tensor:
     C = x.shape[1]
     shape = (1, C) + (1,) * (x.dim() - 2)
-    invstd = torch.rsqrt(bn.running_var.float() + bn.eps)
-    scale = (bn.weight.float() * invstd).reshape(shape)
-    shift = (bn.bias.float() - bn.running_mean.float() * bn.weight.float() * invstd).reshape(shape)
-    y = x.float() * scale + shift
+    invstd = torch.rsqrt(_acc(bn.running_var) + bn.eps)
+    scale = (_acc(bn.weight) * invstd).reshape(shape)
+    shift = (_acc(bn.bias) - _acc(bn.running_mean) * _acc(bn.weight) * invstd).reshape(shape)
+    y = _acc(x) * scale + shift
     if residual is not None:
-        y = y + residual.float()
+        y = y + _acc(residual)
     if relu:
         y = torch.relu(y)
     y = y.to(x.dtype)

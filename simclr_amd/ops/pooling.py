@@ -15,7 +15,7 @@ def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     if registry.use_hip(x) and x.dim() == 4:
         from . import pooling_hip
         return pooling_hip.global_avg_pool(x)
-    return x.float().mean(dim=(2, 3)).to(x.dtype)
+    return (x if x.dtype == torch.float64 else x.float()).mean(dim=(2, 3)).to(x.dtype)
 
 
 class MaxPool2d(nn.Module):

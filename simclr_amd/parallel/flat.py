@@ -44,7 +44,8 @@ def _is_conv_weight(p: torch.Tensor) -> bool:
 class FlatParamStore:
     def __init__(self, model: nn.Module, device: torch.device, shadow_dtype=torch.bfloat16,
                  bucket_mb: float = 32.0, first_bucket_mb: float = 4.0,
-                 group=None, world_size: Optional[int] = None):
+                 group=None, world_size: Optional[int] = None, dtype=torch.float32):
+        # dtype: master / gradient precision (fp32; fp64 only for the CPU equivalence tests)
         self.model = model
         self.device = torch.device(device)
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
@@ -57,14 +58,14 @@ class FlatParamStore:
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.offsets = offs
         self.total = off
-        self.master = torch.zeros(self.total, dtype=torch.float32, device=self.device)
-        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.master = torch.zeros(self.total, dtype=dtype, device=self.device)
+        self.grad = torch.zeros(self.total, dtype=dtype, device=self.device)
         self.shadow = (torch.zeros(self.total, dtype=shadow_dtype, device=self.device)
                        if shadow_dtype is not None else None)
         self.slots: List[ParamSlot] = []
         for i, (p, o) in enumerate(zip(self.params, offs)):
             n = p.numel()
-            src = p.detach().to(self.device, torch.float32)
+            src = p.detach().to(self.device, dtype)
             if _is_conv_weight(p):
                 co, ci, kh, kw = p.shape
                 mview = self.master[o:o + n].view(co, kh, kw, ci)
