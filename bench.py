@@ -115,10 +115,19 @@ def run_ours(args, rank, world, dev):
         _sync(dev, world)
         return time.perf_counter() - t
 
+    def ipc_guard() -> bool:
+        from simclr_amd.comm import fallback_if_failed
+        if fallback_if_failed(st, dev):
+            args.bn_comm = "rccl(ipc-fallback)"
+            return True
+        return False
+
     auto = args.graph == "auto"
     t_eager = None
     if auto and tr.hip:
         timed(2)  # eager warm-up: autotuning, allocator, communicators
+        if ipc_guard():
+            timed(1)
         t_eager = timed(3)
     if args.graph and tr.hip:
         try:
@@ -151,6 +160,12 @@ def run_ours(args, rank, world, dev):
         for _ in range(args.warmup):
             loss = tr.step(next_batch())
         _sync(dev, world)
+        if ipc_guard():  # the captured graph (if any) holds the IPC exchange: issue eagerly
+            tr.graph = None
+            args.graph = False
+            for _ in range(max(1, args.warmup)):
+                loss = tr.step(next_batch())
+            _sync(dev, world)
         t0 = time.perf_counter()
         host = 0.0
         for _ in range(args.steps):

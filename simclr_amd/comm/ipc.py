@@ -192,3 +192,22 @@ def setup_stats_exchange(st, device: torch.device, mode: Optional[str] = None):
         return None
     st.ipc = ex
     return ex
+
+
+def fallback_if_failed(st, device: torch.device) -> bool:
+    """Collective check (call it on every rank, outside any captured region): if a spin of the
+    IPC exchange timed out on some rank — e.g. one rank still autotuning a conv seconds after
+    its peers reached the next BatchNorm — that step's statistics were partial and the sticky
+    error flag makes later exchanges skip waiting.  Every rank then drops to the RCCL path
+    (``st.ipc = None``; the same decision everywhere).  Returns True when it switched; a
+    captured HIP graph holding the exchange must then be discarded by the caller."""
+    if st.ipc is None:
+        return False
+    f = torch.tensor([1 if st.ipc.failed() else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(f, op=dist.ReduceOp.MAX, group=st.group)
+    if int(f.item()) == 0:
+        return False
+    print(f"[ipc] rank {st.rank}: statistics exchange timed out; continuing with RCCL",
+          file=sys.stderr, flush=True)
+    st.ipc = None
+    return True

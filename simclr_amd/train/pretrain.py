@@ -213,6 +213,12 @@ def pretrain(cfg) -> dict:
         if st.device.type == "cuda":
             torch.cuda.synchronize()
         dt = max(time.time() - t0, 1e-9)
+        if st.ipc is not None:
+            from simclr_amd.comm import fallback_if_failed
+            if fallback_if_failed(st, st.device):
+                log.error("epoch %d: IPC BatchNorm-statistics exchange timed out (statistics of "
+                          "that step were partial); switched to RCCL", epoch)
+                tr.graph = None
         imgs = nsteps * cfg["experiment"]["batches"] * st.world_size
         summary.update(epochs_run=summary["epochs_run"] + 1, steps=step_global)
         if rank == 0:

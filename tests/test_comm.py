@@ -32,3 +32,43 @@ def test_no_exchange_on_cpu_or_single_rank():
     import torch
     st = St()
     assert setup_stats_exchange(st, torch.device("cpu")) is None and st.ipc is None
+
+
+def _fallback_worker(rank, world, port, out_dir):
+    import os
+    import torch
+    import torch.distributed as dist
+    from simclr_amd.comm import fallback_if_failed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class FakeExchange:  # stands in for IpcStatsExchange: only rank 1 saw a spin time out
+        def failed(self):
+            return rank == 1
+
+    class St:
+        pass
+    st = St()
+    st.rank, st.group, st.ipc = rank, dist.group.WORLD, FakeExchange()
+    switched = fallback_if_failed(st, torch.device("cpu"))
+    st2 = St()
+    st2.rank, st2.group, st2.ipc = rank, dist.group.WORLD, None
+    untouched = fallback_if_failed(st2, torch.device("cpu"))
+    with open(os.path.join(out_dir, f"fb{rank}"), "w") as f:
+        f.write(f"{int(switched)} {int(st.ipc is None)} {int(untouched)}")
+    dist.destroy_process_group()
+
+
+def test_timeout_fallback_is_collective(tmp_path):
+    """One rank's timed-out exchange switches EVERY rank to RCCL (the decision is all-reduced,
+    so no rank keeps waiting in an exchange its peers abandoned)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_fallback_worker, args=(3, port, str(tmp_path)), nprocs=3, join=True)
+    for r in range(3):
+        assert (tmp_path / f"fb{r}").read_text() == "1 1 0"

@@ -95,6 +95,13 @@ def _worker(rank, world, port, out, fused, ipc=False):
     if ipc:  # BatchNorm statistics through the IPC-mapped arenas (both ranks on cuda:0)
         from simclr_amd.comm import setup_stats_exchange
         assert setup_stats_exchange(st, dev, "ipc") is not None
+    if ipc == "fallback":  # a (simulated) spin timeout on rank 1: every rank drops to RCCL
+        from simclr_amd.comm import fallback_if_failed
+        if rank == 1:
+            st.ipc.err.fill_(1)
+        ex = st.ipc
+        assert fallback_if_failed(st, dev) and st.ipc is None
+        ex.close()
     m, store = _build(dev, fused)
     store.broadcast_from(0)
     v0, v1, w0, w1 = _inputs()
@@ -102,7 +109,7 @@ def _worker(rank, world, port, out, fused, ipc=False):
     x = torch.cat([v0[sl], v1[sl]]).to(dev)
     w = torch.cat([w0[sl], w1[sl]]).to(dev)
     _step(m, store, x, w)
-    if ipc:
+    if st.ipc is not None:
         assert not st.ipc.failed(), "IPC exchange timed out"
     zs = [torch.zeros_like(m._dbg_z) for _ in range(world)]
     dist.all_gather(zs, m._dbg_z)
@@ -118,7 +125,7 @@ def _worker(rank, world, port, out, fused, ipc=False):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("fused,ipc", [(False, False), (True, False), (False, True),
-                                       (True, True)])
+                                       (True, True), (True, "fallback")])
 def test_two_ranks_match_one_process(tmp_path, fused, ipc):
     out = str(tmp_path / "r0.pt")
     ctx = mp.get_context("spawn")
