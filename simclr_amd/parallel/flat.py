@@ -21,7 +21,9 @@ MI355X design:
   statistics (the reference's per-forward broadcast is redundant traffic).
 * Bucket size: default 32 MiB; on MI355X the 7 xGMI links of a GPU give the ring ~7x one link,
   so buckets of tens of MiB amortise RCCL's ~10-20 µs launch floor while the first bucket still
-  starts early in the backward (``first_bucket_mb`` smaller, like DDP's 1 MiB first bucket).
+  starts early in the backward (``first_bucket_mb`` smaller, like DDP's 1 MiB first bucket),
+  and the last one is small (``last_bucket_mb``): its all-reduce is the one left exposed after
+  the backward (see ``_build_buckets``).
 """
 from __future__ import annotations
 
@@ -44,7 +46,7 @@ def _is_conv_weight(p: torch.Tensor) -> bool:
 class FlatParamStore:
     def __init__(self, model: nn.Module, device: torch.device, shadow_dtype=torch.bfloat16,
                  bucket_mb: float = 32.0, first_bucket_mb: float = 4.0,
-                 group=None, world_size: Optional[int] = None, dtype=torch.float32):
+                 last_bucket_mb: float = 2.0, group=None, world_size: Optional[int] = None, dtype=torch.float32):
         # dtype: master / gradient precision (fp32; fp64 only for the CPU equivalence tests)
         self.model = model
         self.device = torch.device(device)
@@ -90,7 +92,7 @@ class FlatParamStore:
         self.group = group if group is not None else st.group
         self.world_size = world_size if world_size is not None else st.world_size
         self.comm = self.world_size > 1 or (world_size is None and group is None and st.comm)
-        self._build_buckets(bucket_mb, first_bucket_mb)
+        self._build_buckets(bucket_mb, first_bucket_mb, last_bucket_mb)
         self._comm_stream = None
         # streams that write gradients (the fused executor adds its weight-gradient stream):
         # a bucket's all-reduce waits for all of them
@@ -118,23 +120,43 @@ class FlatParamStore:
         return [(o, p.numel()) for o, p in zip(self.offsets, self.params)]
 
     # ------------------------------------------------------------------ reducer
-    def _build_buckets(self, bucket_mb: float, first_bucket_mb: float) -> None:
-        cap_first = int(first_bucket_mb * 1024 * 1024 / 4)
-        cap = int(bucket_mb * 1024 * 1024 / 4)
-        self.bucket_of: List[int] = []
+    def _build_buckets(self, bucket_mb: float, first_bucket_mb: float,
+                       last_bucket_mb: float) -> None:
+        """Front: one ``first_bucket_mb`` bucket (the head's gradients, ready first).  The rest
+        is cut from the BACK: a small ``last_bucket_mb`` bucket (stem + layer1, the last
+        gradients of the backward, whose all-reduce cannot overlap anything) and ``bucket_mb``
+        buckets before it.  Cutting front-to-back instead leaves whatever remains — 16 MiB of
+        layer2/layer3 gradients for ResNet-50 at 32 MiB buckets — waiting for the stem's
+        gradient and then all-reduced after the backward, fully exposed."""
+        mib = 1024 * 1024 / 4
+        cap_first, cap = int(first_bucket_mb * mib), int(bucket_mb * mib)
+        cap_last = int(last_bucket_mb * mib) if last_bucket_mb > 0 else cap
+        sizes = [(p.numel() + ALIGN - 1) // ALIGN * ALIGN for p in self.params]
+        P = len(sizes)
+        groups: List[Tuple[int, int]] = []  # [i0, i1) param index ranges, in order
+        i1, size = 0, 0
+        while i1 < P and (i1 == 0 or size + sizes[i1] <= cap_first):
+            size += sizes[i1]
+            i1 += 1
+        if i1 > 0:
+            groups.append((0, i1))
+        tail: List[Tuple[int, int]] = []
+        end, size = P, 0
+        for i in range(P - 1, i1 - 1, -1):
+            limit = cap_last if not tail else cap
+            if end - (i + 1) > 0 and size + sizes[i] > limit:
+                tail.append((i + 1, end))
+                end, size = i + 1, 0
+            size += sizes[i]
+        if end > i1:
+            tail.append((i1, end))
+        groups += reversed(tail)
+        self.bucket_of: List[int] = [0] * P
         self.buckets: List[Tuple[int, int, int]] = []  # (beg, end, n_params)
-        beg, count, size = 0, 0, 0
-        for i, p in enumerate(self.params):
-            limit = cap_first if not self.buckets else cap
-            n = (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-            if count > 0 and size + n > limit:
-                self.buckets.append((beg, self.offsets[i], count))
-                beg, count, size = self.offsets[i], 0, 0
-            self.bucket_of.append(len(self.buckets))
-            count += 1
-            size += n
-        if count > 0:
-            self.buckets.append((beg, self.total, count))
+        for b, (a, z) in enumerate(groups):
+            for i in range(a, z):
+                self.bucket_of[i] = b
+            self.buckets.append((self.offsets[a], self.offsets[z] if z < P else self.total, z - a))
 
     def reset_step(self) -> None:
         self._ready = [0] * len(self.buckets)

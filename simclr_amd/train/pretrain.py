@@ -50,7 +50,8 @@ def build_contrastive_model(cfg, device, precision: str):
     model = model.to(device)
     shadow = torch.bfloat16 if (precision == "bf16" and device.type == "cuda") else None
     store = FlatParamStore(model, device, shadow_dtype=shadow,
-                           bucket_mb=cfg_get(cfg, "runtime.bucket_mb", 32.0))
+                           bucket_mb=cfg_get(cfg, "runtime.bucket_mb", 32.0),
+                           last_bucket_mb=cfg_get(cfg, "runtime.last_bucket_mb", 2.0))
     store.broadcast_from(0)
     return model, store
 

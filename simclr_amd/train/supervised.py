@@ -83,7 +83,8 @@ def supervised(cfg) -> dict:
                             stem_padding=cfg_get(cfg, "model.stem_padding", 3)).to(dev)
     store = FlatParamStore(model, dev,
                            shadow_dtype=torch.bfloat16 if precision == "bf16" and dev.type == "cuda"
-                           else None, bucket_mb=cfg_get(cfg, "runtime.bucket_mb", 32.0))
+                           else None, bucket_mb=cfg_get(cfg, "runtime.bucket_mb", 32.0),
+                           last_bucket_mb=cfg_get(cfg, "runtime.last_bucket_mb", 2.0))
     store.broadcast_from(0)
     steps_per_epoch = max(1, int(len(train_ds) / (bs * st.world_size)))
     epochs = cfg["parameter"]["epochs"]

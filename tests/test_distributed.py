@@ -169,3 +169,25 @@ def test_launcher_env_and_overrides():
     assert c1[-3:] == ["distributed.local_rank=1", "distributed.world_size=4",
                        "parameter.epochs=1"]
     assert c0[1:4] == ["-u", "-m", "main"]
+
+
+@pytest.mark.parametrize("base,stem", [("resnet50", True), ("resnet18", None)])
+def test_bucket_layout(base, stem):
+    """Buckets tile the flat gradient contiguously in backward order; the first holds the head,
+    the last (stem + layer1: the only all-reduce left exposed after the backward) is small."""
+    from simclr_amd.models import ContrastiveModel
+    from simclr_amd.parallel import state as pstate
+    from simclr_amd.parallel.flat import FlatParamStore
+    pstate.reset()
+    m = ContrastiveModel(base, cifar_stem=stem)
+    st = FlatParamStore(m, "cpu", shadow_dtype=None, bucket_mb=32.0, first_bucket_mb=4.0,
+                        last_bucket_mb=2.0)
+    assert st.buckets[0][0] == 0 and st.buckets[-1][1] == st.total
+    for (b0, e0, _), (b1, _, _) in zip(st.buckets, st.buckets[1:]):
+        assert e0 == b1
+    assert sum(c for _, _, c in st.buckets) == len(st.params)
+    assert st.bucket_of == sorted(st.bucket_of)
+    mib = [(e - b) * 4 / 2 ** 20 for b, e, _ in st.buckets]
+    assert mib[-1] <= 2.0 and mib[0] <= 4.0 and max(mib) <= 32.0, mib
+    assert st.names[-1] == "f.conv1.weight" and st.bucket_of[-1] == len(st.buckets) - 1
+    assert st.names[0].startswith("g.")
