@@ -198,6 +198,9 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const std::vector<c10::optional<Tensor>>& tail_t, std::vector<double> tail_f,
            std::vector<int64_t> tail_i, int64_t stats_groups) {
   const ConvGeom g = geom_from(gv);
+  // bit 8 of epi_mode: epi_a is the stride-2 subsampled residual (conv.hip epi_load_batch)
+  const bool epi_sub = (epi_mode & 256) != 0;
+  epi_mode &= 255;
   TORCH_CHECK(A.numel() == (int64_t)g.Nb * g.IH * g.IW * g.C, "igemm: A numel mismatch");
   TORCH_CHECK(A.numel() * 2 < (int64_t)1 << 31, "igemm: A larger than 2 GiB");
   const int64_t K = (int64_t)g.KH * g.KW * g.C;
@@ -223,8 +226,21 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   const bool has_stats = stats.has_value() && stats->defined();
   if (has_stats && stats_seg_blocks == 0 && stats_groups == 0)
     TORCH_CHECK(stats->numel() >= ((M + bm - 1) / bm) * 2 * g.N, "igemm: stats buffer too small");
+  const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
+                      g.OWp == g.OW;
+  const int64_t sub_numel = (int64_t)g.Nb * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) * g.ldo;
+  if (epi_sub) {
+    TORCH_CHECK(epi_mode == 1 || epi_mode == 2 || epi_mode == 4,
+                "igemm: a subsampled residual needs epilogue mode 1, 2 or 4");
+    TORCH_CHECK(direct, "igemm: a subsampled residual needs a direct (stride-1) output");
+    TORCH_CHECK(epi_a.has_value() && epi_a->defined() && epi_a->numel() == sub_numel,
+                "igemm: subsampled residual must be [Nb][ceil(OH/2)][ceil(OW/2)][ldo]");
+  }
   ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, 1, epi_mode, epi_a, epi_b,
-                             g.C, out.numel());
+                             g.C, epi_sub ? sub_numel : out.numel());
+  f.epi_a_sub = epi_sub ? 1 : 0;
+  if (epi_sub && epi_mode == 2)
+    TORCH_CHECK(epi_b->numel() >= out.numel(), "epilogue operand b");
   f.seg_rows = (int)seg_rows;
   f.stats_seg_blocks = (int)stats_seg_blocks;
   f.stats_base = (int)stats_base;

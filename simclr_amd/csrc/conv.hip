@@ -67,6 +67,7 @@ struct IgemmArgs {
   //   the block-input gradient of a residual block, already masked by the previous block's
   //   output ReLU, with that block's last-BN backward reduce folded in
   int epi_mode;
+  int epi_a_sub;  // epi_a: stride-2 subsampled residual (direct output only), see ConvFusion
   const uint16_t* epi_a;
   const uint16_t* epi_b;
   const uint16_t* epi_c;
@@ -160,7 +161,23 @@ __device__ __forceinline__ void epi_load_batch(const IgemmArgs& p, int m0, int n
     }
     b.o[u] = b.ok[u] ? oo : 0;  // a dead lane reads element 0 and stores nothing
     // streamed operands: read once, nontemporal (no L2 allocation for 0.1-0.5 GB tensors)
-    if (EA) b.ea[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_a + b.o[u]));
+    if (EA) {
+      if (p.epi_a_sub) {
+        // the residual lives only at even (oh, ow): a stride-2 1x1 downsample's dgrad, kept
+        // compact instead of zero-filling the full-resolution tensor (host: direct output)
+        const int img = m / OHW;
+        const int rem = m - img * OHW;
+        const int oh = rem / p.OW;
+        const int ow = rem - oh * p.OW;
+        const bool on = b.ok[u] && !((oh | ow) & 1);
+        const size_t oc = ((size_t)(img * ((p.OH + 1) >> 1) + (oh >> 1)) * ((p.OW + 1) >> 1) +
+                           (ow >> 1)) * p.ldo + n;
+        b.ea[u] = on ? __builtin_nontemporal_load((const u32x4*)(p.epi_a + oc))
+                     : (u32x4){0u, 0u, 0u, 0u};
+      } else {
+        b.ea[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_a + b.o[u]));
+      }
+    }
     if (EC) b.ec[u] = __builtin_nontemporal_load((const u32x4*)(p.epi_c + b.o[u]));
     if (two) b.ec2[u] = *(const u32x4*)(p.epi_c2 + b.o[u]);
     if (EB) {
@@ -1994,7 +2011,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.pro_relu = f.pro_relu;
   a.pro_d = f.pro_d; a.A2 = f.A2;
   a.pro_rsc = f.pro_rsc; a.pro_rsh = f.pro_rsh; a.pro_out = f.pro_out; a.pro_mask = f.pro_mask;
-  a.epi_mode = f.epi_mode; a.epi_a = f.epi_a; a.epi_b = f.epi_b; a.epi_c = f.epi_c;
+  a.epi_mode = f.epi_mode; a.epi_a_sub = f.epi_a_sub; a.epi_a = f.epi_a; a.epi_b = f.epi_b; a.epi_c = f.epi_c;
   a.epi_mask = f.epi_mask;
   a.epi_c2 = f.epi_c2; a.epi_mi2 = f.epi_mi2; a.stats2 = f.stats2;
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;

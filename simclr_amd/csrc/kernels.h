@@ -68,6 +68,8 @@ struct ConvFusion {
   const float* dp_coef = nullptr;
   int dp_seg_rows = 0, dp_S = 1;
   int epi_mode = 0;               // igemm: 1 out = acc + a; 2 out = acc + (b > 0 ? a : 0);
+  int epi_a_sub = 0;              // epi_a is the stride-2 subsampled [Nb][ceil(OH/2)][ceil(OW/2)][ldo]
+                                  // tensor (a stride-2 1x1 downsample's compact dgrad): 0 at odd (oh, ow)
                                   // 3 out = (b*sc+sh > 0 ? acc : 0) + BN-bwd partials
                                   // 4 out = (b > 0 ? acc + a : 0) + BN-bwd partials vs c
   const uint16_t* epi_a = nullptr;

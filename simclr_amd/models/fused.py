@@ -112,6 +112,10 @@ class _BlockTape:
     mask: Optional[torch.Tensor] = None  # uint8 ReLU bitmask of ``out`` (bit per channel)
 
 
+# bit 8 of the igemm epilogue mode: the residual operand is stride-2 subsampled (conv.hip)
+_EPI_SUB = 256
+
+
 class FusedStages:
     """Executor over ``resnet.layer1..layer4`` (modules stay the parameter / state owners)."""
 
@@ -133,6 +137,11 @@ class FusedStages:
         # the downsample branch of a stage's first block (forward conv + BN, backward dgrad) on
         # its own stream, concurrent with the main branch until the block output / conv1 dgrad
         self.branch_stream = os.environ.get("SIMCLR_BRANCH_STREAM", "1") != "0"
+        # a stride-2 1x1 downsample's dgrad is kept compact ([N, H/2, W/2, C]: it only reaches
+        # the even positions) and added by conv1's dgrad epilogue through the subsampled-residual
+        # mode — instead of zero-filling a full-resolution tensor (0.9 GB/step of fills at
+        # ResNet-50 CIFAR) and re-reading it whole
+        self.compact_ds = os.environ.get("SIMCLR_COMPACT_DS", "1") != "0"
         self._branch = None
         # a block's output (BN3 + shortcut + ReLU) formed inside the next block's conv1 prologue
         # instead of a separate pass that conv1 re-reads.  SIMCLR_BLOCK_OUT_PROLOGUE: 0 = off,
@@ -465,7 +474,8 @@ class FusedStages:
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
                dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,
                bnb: Optional[Tuple] = None, tail_bn: Optional[Tuple] = None,
-               acc_keys: Optional[Tuple] = None):
+               acc_keys: Optional[Tuple] = None, compact: bool = False,
+               sub_resid: bool = False):
         """dx (NHWC) = conv-transpose(dy).  ``accumulate``: dx += result (dx must be given).
 
         ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
@@ -484,12 +494,30 @@ class FusedStages:
         ``tail_bn = (bn, bn_state, st)``: when the partials come from ONE launch (stride 1, no
         second BN stream) its last blocks also finalize that BatchNorm's backward — the
         partials entry of the result is then ("tail", coef) with dγ, dβ already delivered.
+        ``compact`` (stride-2 1x1, pad 0): return the dgrad only at the even input positions, as
+        a dense [N, ceil(H/2), ceil(W/2), Ci] tensor (one stride-1 GEMM, no zero fill).
+        ``sub_resid``: the residual (``dx`` with ``accumulate``, or bn_epi's resid) is such a
+        compact tensor; the epilogue adds it at the even positions and dx is a new tensor.
         """
         Nb, H, W, Ci = in_shape
         _, OH, OW, Co = dyn.shape
         KH = KW = cs.k
         dev = dyn.device
         w = shadow_ohwi(cs.conv.weight, Ci)
+        if compact:
+            assert cs.stride == 2 and KH == 1 and cs.pad == 0 and bn_epi is None
+            assert not accumulate and (OH, OW) == ((H + 1) // 2, (W + 1) // 2)
+            dc = _empty_nhwc(Nb, OH, OW, Ci, dev)
+            wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, 2, 0, 2])
+            g = [Nb, OH, OW, Co, OH, OW, 1, 1, 1, 1, 1, 1, 0, 0, Ci, OH, OW, 1, 1, 0, 0, Ci]
+            v = igemm_choose(ops, dyn, wt, dc, g)
+            igemm_launch(ops, dyn, wt, dc, g, v)
+            return dc, None, 0
+        resid_c = None
+        if sub_resid:
+            assert cs.stride == 1 and (accumulate or bn_epi is not None)
+            resid_c = dx if bn_epi is None else bn_epi[1]
+            dx = None  # the full-resolution result is a new tensor
         if dx is None:
             dx = _empty_nhwc(Nb, H, W, Ci, dev)
         launches = []
@@ -526,6 +554,8 @@ class FusedStages:
                     dx.zero_()
         if bn_epi is None:
             epi = (1, dx, None) if accumulate else None
+            if resid_c is not None:
+                epi = (1 | _EPI_SUB, resid_c, None)
             for wt, g, M in launches:
                 v = igemm_choose(ops, dyn, wt, dx, g, epi=epi)
                 igemm_launch(ops, dyn, wt, dx, g, v, epi=epi)
@@ -537,7 +567,7 @@ class FusedStages:
             tables = (bs.ss.view(-1), bs.mi)
         else:
             _, resid, mask, a_prev, mi, ad_prev, mid_prev = bn_epi
-            epi = (4, resid, None, a_prev, mask)
+            epi = (4 | (_EPI_SUB if resid_c is not None else 0), resid, None, a_prev, mask)
             tables = (None, mi)
         chosen = []
         bpro = None
@@ -840,13 +870,17 @@ class FusedStages:
                 else:
                     ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
         resid_f = None
+        # (bottleneck blocks: conv1 is 1x1 stride 1, so its dgrad epilogue covers every input
+        # position; a BasicBlock's conv1 carries the stride itself)
+        compact = (b.down is not None and self.compact_ds and b.down.stride == 2 and b.down.k == 1
+                   and b.down.pad == 0 and b.convs[0].stride == 1)
         br = self._branch_stream(dad) if dad is not None else None
         if br is not None:
             # the downsample dgrad only meets the conv chain at conv1's dgrad epilogue
             br.wait_stream(torch.cuda.current_stream(dad.device))
             with torch.cuda.stream(br):
                 _ext.TAG = f"{b.name} ds dgrad"
-                resid_f, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
+                resid_f, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S, compact=compact)
         # conv chain, last to first: dgrad (+ BN-bwd partials) → start BN all-reduce → wgrad →
         # finish BN → apply
         for i in range(L, 0, -1):
@@ -874,18 +908,20 @@ class FusedStages:
                 resid = resid_f
             else:
                 _ext.TAG = f"{b.name} ds dgrad"
-                resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S)
+                resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S, compact=compact)
         else:
             resid = g3
         _ext.TAG = f"{b.name} conv1 dgrad"
         if prev is None:
-            dx, _, _ = self._dgrad(ops, da, cs0, tp.x.shape, S, accumulate=True, dx=resid)
+            dx, _, _ = self._dgrad(ops, da, cs0, tp.x.shape, S, accumulate=True, dx=resid,
+                                   sub_resid=compact)
             h = None
         else:
             pb, ptp = prev
             pds = pb.down is not None
             dx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S,
-                                       dx=resid if b.down is not None else None,
+                                       dx=resid if b.down is not None and not compact else None,
+                                       sub_resid=compact,
                                        bn_epi=("res", resid, ptp.mask, ptp.acts[-1],
                                                ptp.bns[-1].mi, ptp.ad if pds else None,
                                                ptp.bnd.mi if pds else None),

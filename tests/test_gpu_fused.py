@@ -305,3 +305,53 @@ def test_weight_transform_batch_matches_single(ops):
     ops.weight_transform_batch(plan[:-1].to(DEV), int(plan[-1]))
     for got, ref in zip(Wts, refs):
         assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("H,mode", [(16, 1), (7, 1), (16, 4)])
+def test_compact_downsample_residual(ops, H, mode):
+    """A stride-2 1x1 downsample's dgrad kept compact ([N, ceil(H/2), ceil(W/2), C], one
+    stride-1 GEMM) and added by conv1's dgrad epilogue through the subsampled-residual mode
+    (epi_mode | 256) == the zero-filled full-resolution residual, bitwise: the same bf16
+    values are added at the even positions, nothing elsewhere."""
+    from simclr_amd.models.fused import FusedStages, _BNState, _ConvSpec
+    torch.manual_seed(11)
+    N, Cin, Cmid, Cds, S = 8, 64, 64, 128, 2
+    conv1 = torch.nn.Conv2d(Cin, Cmid, 1, 1, 0, bias=False).to(DEV)
+    down = torch.nn.Conv2d(Cin, Cds, 1, 2, 0, bias=False).to(DEV)
+    for c in (conv1, down):
+        with torch.no_grad():
+            c.weight.copy_(_bf(torch.randn_like(c.weight) * 0.1).float())
+    OHd = (H + 1) // 2
+    da = _bf(torch.randn(N, H, H, Cmid, device=DEV))       # conv1 output gradient
+    dad = _bf(torch.randn(N, OHd, OHd, Cds, device=DEV))   # downsample output gradient
+    ex = FusedStages.__new__(FusedStages)
+    cs1, csd = _ConvSpec(conv1, None, 1, 1, 0), _ConvSpec(down, None, 2, 1, 0)
+    shape = (N, H, H, Cin)
+    full, _, _ = ex._dgrad(ops, dad, csd, shape, S)                 # zero-filled, full size
+    comp, _, _ = ex._dgrad(ops, dad, csd, shape, S, compact=True)   # even positions only
+    assert comp.shape == (N, OHd, OHd, Cin)
+    assert torch.equal(full[:, ::2, ::2], comp)
+    if mode == 1:
+        ref, _, _ = ex._dgrad(ops, da, cs1, shape, S, accumulate=True, dx=full.clone())
+        got, _, _ = ex._dgrad(ops, da, cs1, shape, S, accumulate=True, dx=comp, sub_resid=True)
+        assert torch.equal(got, ref)
+        return
+    # mode 4: g = (dgrad + resid)·[y > 0] with the BatchNorm-backward partials of the producer
+    y = _bf(torch.randn(N, H, H, Cin, device=DEV))
+    mask = torch.zeros(N * H * H * Cin // 8, dtype=torch.uint8, device=DEV)
+    bits = (y.reshape(-1, 8) > 0).to(torch.uint8) << torch.arange(8, device=DEV, dtype=torch.uint8)
+    mask.copy_(bits.sum(1).to(torch.uint8))
+    a_prev = _bf(torch.randn(N, H, H, Cin, device=DEV))
+    mi = torch.cat([torch.randn(S, Cin, device=DEV) * 0.1,
+                    torch.rand(S, Cin, device=DEV) + 0.5]).reshape(-1).contiguous()
+    outs = []
+    for sub in (False, True):
+        res = comp if sub else full.clone()
+        gx, part, nb = ex._dgrad(ops, da, cs1, shape, S, dx=None if sub else res,
+                                 sub_resid=sub,
+                                 bn_epi=("res", res, mask, a_prev, mi, None, None))
+        sums = torch.empty(2 * S * Cin, device=DEV)
+        ops.bn_reduce(part, nb, S, Cin, sums)
+        outs.append((gx, sums))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5)
