@@ -219,8 +219,8 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   } else if (igemm_variant_glds((int)variant)) {
     TORCH_CHECK(igemm_variant_ok((int)variant, g, pro_sc.has_value() && pro_sc->defined(),
                                  pro_d.has_value() && pro_d->defined()),
-                "igemm: LDS-DMA variant needs C % 64 == 0, no BN-backward prologue, and a BN-apply "
-                "prologue only on unpadded 1x1 convolutions");
+                "igemm: LDS-DMA variant needs C % 64 == 0 and its prologues (BN-apply, "
+                "BN-backward) only on unpadded 1x1 convolutions (2-stage tiles whose staging fits)");
   }
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
   const bool has_stats = stats.has_value() && stats->defined();

@@ -749,10 +749,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "glds tiling");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int stages = p.K > 64 ? NST : 1;
-  constexpr int NA = PRO == 3 ? 2 : 1;
+  constexpr int NA = PRO >= 2 ? 2 : 1;  // PRO 2 / 3 stage a second A-shaped operand (Rs)
   uint16_t* As = (uint16_t*)smem;          // [stages][BM][64]
   uint16_t* Bs = As + stages * BM * 64;    // [stages][BN][64] (one stage when K <= 64)
-  uint16_t* Rs = Bs + stages * BN * 64;    // PRO 3: [stages][BM][64] residual tile
+  uint16_t* Rs = Bs + stages * BN * 64;    // PRO 3: residual / PRO 2: A2 tile, [stages][BM][64]
   // PRO: [sc, sh (, rsc, rsh)][C] of the block's segment, behind the staging buffers and the
   // epilogue image
   float* Pt = (float*)(smem + igemm_glds_pro_offset(BM, BN, 64 * WM * WN, stages, NA));
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(PRO == 3 ? p.A2 : p.A), (short)0, (int)p.a_bytes, 0x00020000);
+      (void*)(PRO >= 2 ? p.A2 : p.A), (short)0, (int)p.a_bytes, 0x00020000);
 
   // lane → (row within its 8-row piece, physical chunk); the logical chunk it fetches is
   // pch ^ (row & 7) = pch ^ lrow (every piece starts at a multiple of 8 rows)
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       // after its issue (see dma16_opaque), so those kernels issue it opaquely
       if (PRO) {
         dma16_opaque(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
-        if (PRO == 3) dma16_opaque(rr, Rs + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+        if (PRO >= 2) dma16_opaque(rr, Rs + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
       } else {
         dma16(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
       }
@@ -844,6 +844,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     const int pseg = m0 / p.pro_seg_rows;  // block-uniform (host guarantees)
     for (int i = tid; i < 2 * p.C; i += NT)
       Pt[i] = (i < p.C ? p.pro_sc : p.pro_sh)[pseg * p.C + (i < p.C ? i : i - p.C)];
+    if (PRO == 2)  // BN-backward: a = sc·A + sh·A2 + d, the d column after sc, sh
+      for (int i = tid; i < p.C; i += NT) Pt[2 * p.C + i] = p.pro_d[pseg * p.C + i];
     if (PRO == 3)  // residual scale / shift; identity residual = (1, 0)
       for (int i = tid; i < 2 * p.C; i += NT) {
         const int c = i < p.C ? i : i - p.C;
@@ -909,6 +911,30 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
           for (int e = 0; e < 8; ++e) bits |= (o[e] > 0.f ? 1u : 0u) << e;
           p.pro_mask[o8 / 8] = (uint8_t)bits;
         }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else if (PRO == 2) {
+      // BatchNorm backward of the layer this conv's dgrad consumes, on the landed tiles: the
+      // DMA brought dY (As) and the pre-BN activation (Rs); the GEMM operand is
+      // A·dY + B·x + D (1x1 unpadded only: no padding taps, K = C)
+      const int ci0 = kt * 64;
+#pragma unroll
+      for (int i = 0; i < BM * 8 / NT; ++i) {
+        const int c = tid + i * NT;
+        const int row = c >> 3, lc = (c & 7) ^ (row & 7);
+        const int ci = ci0 + lc * 8;
+        u32x4* q = (u32x4*)(As + cur * BM * 64 + c * 8);
+        const u32x4 r = *(const u32x4*)(Rs + cur * BM * 64 + c * 8);
+        float tb[3][8];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const float4* pt = (const float4*)(Pt + t * p.C + ci);
+          const float4 t0 = pt[0], t1 = pt[1];
+          tb[t][0] = t0.x; tb[t][1] = t0.y; tb[t][2] = t0.z; tb[t][3] = t0.w;
+          tb[t][4] = t1.x; tb[t][5] = t1.y; tb[t][6] = t1.z; tb[t][7] = t1.w;
+        }
+        *q = bnbwd8(*q, r, tb[0], tb[1], tb[2], true);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1767,8 +1793,8 @@ void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
-  const size_t lds = igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? NST : 1, PRO == 3 ? 2 : 1) +
-                     (PRO ? (size_t)(PRO == 3 ? 4 : 2) * a.C * 4 : 0);
+  const size_t lds = igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? NST : 1, PRO >= 2 ? 2 : 1) +
+                     (PRO ? (size_t)(PRO == 3 ? 4 : PRO == 2 ? 3 : 2) * a.C * 4 : 0);
   hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI, NST>), dim3(a.nMb * a.nNb), dim3(NT),
                      lds, s, a);
   HIP_CHECK_LAUNCH();
@@ -1811,6 +1837,18 @@ void launch_patch(const IgemmArgs& a, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, int NST = 2>
 void launch_glds(const IgemmArgs& a, hipStream_t s) {
+  if (a.pro_d != nullptr) {  // BN-backward prologue (PRO 2): plain or mode-3 epilogue
+    if constexpr (NST == 2) {
+      if (a.epi_mode == 3)
+        launch_glds_t<BM, BN, WM, WN, 2, 3, NST>(a, s);
+      else
+        launch_glds_t<BM, BN, WM, WN, 2, 0, NST>(a, s);
+    } else {
+      fprintf(stderr, "igemm: 3-stage LDS-DMA variant with the BN-backward prologue\n");
+      abort();
+    }
+    return;
+  }
   if (a.pro_out != nullptr) {  // block-output prologue: 2 stages, plain epilogue (host-checked)
     if constexpr (NST == 2) {
       launch_glds_t<BM, BN, WM, WN, 3, 0, NST>(a, s);
@@ -1957,9 +1995,10 @@ int igemm_variant_bn(int v) { return IG_VARIANTS[v][1]; }
 int igemm_default_variant(int N) { return N <= 64 ? 1 : 0; }
 bool igemm_variant_glds(int v) { return v >= IG_GLDS0 && v < igemm_num_variants(); }
 bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro) {
-  if (g.C % 64 != 0 || bn_bwd_pro) return false;
-  // the BN-apply prologue runs on the landed tile: only valid without zero-padding taps
-  return !pro || (g.KH == 1 && g.KW == 1 && g.ih0 == 0 && g.iw0 == 0);
+  if (g.C % 64 != 0) return false;
+  // the BN-apply / BN-backward prologues run on the landed tile: only valid without
+  // zero-padding taps
+  return !(pro || bn_bwd_pro) || (g.KH == 1 && g.KW == 1 && g.ih0 == 0 && g.iw0 == 0);
 }
 bool igemm_patch_ok(const ConvGeom& g) {
   const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
@@ -1987,7 +2026,12 @@ bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
   if (v >= IG_PATCH0 && v < IG_GLDS8W) return !pro && !bn_bwd_pro && igemm_patch_ok(g);
-  if (v >= IG_GLDS3 && v < IG_PATCH0 && pro) return false;
+  if (v >= IG_GLDS3 && v < IG_PATCH0 && (pro || bn_bwd_pro)) return false;
+  if (bn_bwd_pro) {  // PRO 2 stages dY and x: doubled A staging + a 3 x C table must fit
+    const int BM = IG_VARIANTS[v][0], BN = IG_VARIANTS[v][1];
+    const size_t lds = igemm_glds_pro_offset(BM, BN, 512, g.C > 64 ? 2 : 1, 2) + (size_t)12 * g.C;
+    if (lds > 160 * 1024) return false;
+  }
   return igemm_glds_ok(g, pro, bn_bwd_pro);
 }
 int igemm_block_m(int N) { return igemm_variant_bm(igemm_default_variant(N)); }
@@ -2061,7 +2105,8 @@ bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < wgrad_num_variants(
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
   if (v >= WG_PATCH0) return !pro && !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
-  return v < WG_GLDS0 || igemm_glds_ok(g, pro, dy_pro);
+  // wgrad_glds has the X-operand BN-apply prologue only (no dY BN-backward prologue)
+  return v < WG_GLDS0 || (!dy_pro && igemm_glds_ok(g, pro, false));
 }
 
 int wgrad_splits(const ConvGeom& g, int variant) {

@@ -129,6 +129,7 @@ class FusedStages:
         self.out_apply_calls = 0
         # BN backward of a bottleneck's conv3 inside conv3's dgrad/wgrad operand prologues
         self.bnb_prologue = os.environ.get("SIMCLR_BNB_PROLOGUE", "1") != "0"
+        self._bnb_max_cin = int(os.environ.get("SIMCLR_BNB_MAX_CIN", "128"))
         # weight gradients on a second stream (forked after each conv's dY is final, joined at
         # the end of the backward): they only feed the flat gradient buffer, so they overlap the
         # dgrad / BatchNorm chain that the next layer's gradient depends on
@@ -469,7 +470,7 @@ class FusedStages:
         (measured on layer3/layer4 of ResNet-50: net loss or break-even)."""
         M = a.numel() // a.shape[-1]
         return (self.bnb_prologue and cs.k == 1 and cs.stride == 1 and M % S == 0
-                and (M // S) % 256 == 0 and cs.conv.in_channels <= 128)
+                and (M // S) % 256 == 0 and cs.conv.in_channels <= getattr(self, "_bnb_max_cin", 128))
 
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
                dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,

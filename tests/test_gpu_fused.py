@@ -355,3 +355,35 @@ def test_compact_downsample_residual(ops, H, mode):
         outs.append((gx, sums))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,H,Ci,Co", [(8, 16, 64, 256), (16, 8, 128, 512)])
+def test_bn_backward_prologue_every_variant(ops, N, H, Ci, Co):
+    """Every admissible tile variant of the 1x1 dgrad with the BN-backward operand prologue —
+    the register-staged kernel and the LDS-DMA kernel (PRO 2: dY and x both DMA'd, the
+    prologue applied on the landed tiles) — equals the dgrad of the materialised
+    da = A·dY + B·x + D."""
+    from simclr_amd.ops.conv_hip import fwd_geom  # noqa: F401  (geometry layout reference)
+    torch.manual_seed(9)
+    S = 2
+    M = N * H * H
+    g = _bf(torch.randn(N, H, H, Co, device=DEV))
+    a = _bf(torch.randn(N, H, H, Co, device=DEV))
+    coef = torch.randn(3 * S * Co, device=DEV) * 0.5
+    wt = _bf(torch.randn(Ci, Co, device=DEV) / math.sqrt(Co)).contiguous()  # dgrad B = W^T
+    da = torch.empty_like(a)
+    ops.bn_bwd_apply(g, None, a, coef, S, False, da, None)
+    geom = [N, H, H, Co, H, H, 1, 1, 1, 1, 1, 1, 0, 0, Ci, H, H, 1, 1, 0, 0, Ci]
+    ref = torch.empty(N, H, H, Ci, device=DEV, dtype=torch.bfloat16)
+    ops.igemm(da, wt, ref, None, None, geom, None, None, 0, False, 0, None, None, 0)
+    c = coef.view(3, S * Co)
+    seen_glds = False
+    for v in range(ops.igemm_nvariants()):
+        if not ops.igemm_variant_ok(v, geom, True, True) or (M // S) % ops.igemm_variant_bm(v):
+            continue
+        out = torch.empty_like(ref)
+        ops.igemm(g, wt, out, None, None, geom, c[0], c[1], M // S, False, 0, None, None, v,
+                  None, None, 0, 0, 0, None, None, None, None, None, c[2], a, None, None, None)
+        assert _rel(out, ref) < 1e-2, v
+        seen_glds |= ops.igemm_variant_glds(v)
+    assert seen_glds, "no LDS-DMA variant admitted the BN-backward prologue"
