@@ -996,8 +996,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
 // patch at shifted pixel positions; only the weight tile streams per k-step (2 LDS stages).
 // Patch image: [pixel][C] with 16-byte chunk c of pixel q stored at chunk c ^ (q & 7).
 // Host guarantees (igemm_variant_ok): KH = KW = 3, unit strides, ih0 = iw0 = -1, OH = IH,
-// OW = IW in {16, 32}, C in {64, 128}, direct output, no prologue.
-template <int BN, int WM, int WN, int EPI>
+// OW = IW in {16, 32}, C in {64, 128}, direct output; PRO 1 (BN-apply + ReLU on the landed
+// patch, padding kept zero) only with the plain epilogue.
+template <int BN, int WM, int WN, int EPI, int PRO>
 __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
   constexpr int BM = 256;
   constexpr int NW = WM * WN, NT = 64 * NW;
@@ -1078,6 +1079,29 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch (first step) + weight tile kt
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    if (PRO && kt == 0) {
+      // the previous BatchNorm's normalise + ReLU, once per patch pixel on the landed patch
+      // (no DMA in flight here); the zero padding of out-of-image pixels stays exactly zero
+      const int pseg = m0 / p.pro_seg_rows;  // block-uniform (host guarantees)
+      const float* psc = p.pro_sc + pseg * C;
+      const float* psh = p.pro_sh + pseg * C;
+      for (int c = tid; c < PP * CPP; c += NT) {
+        const int q = c / CPP, pch = c - q * CPP;
+        const int pr = q / PW, pc = q - pr * PW;
+        const int ih = row0 - 1 + pr, iw = pc - 1;
+        if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
+          const int ch = (pch ^ (q & 7)) * 8;
+          const float4 s0 = *(const float4*)(psc + ch), s1 = *(const float4*)(psc + ch + 4);
+          const float4 h0 = *(const float4*)(psh + ch), h1 = *(const float4*)(psh + ch + 4);
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+          u32x4* ptr = (u32x4*)(Ps + q * C + pch * 8);
+          *ptr = affine_relu8(*ptr, sc, sh, true, p.pro_relu != 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     if (kt + 1 < nk) issue_b(kt + 1, cur ^ 1);
     const int k0 = kt * 64;
     const int tap = k0 / C;
@@ -1546,7 +1570,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
 // t from them — the implicit GEMM's per-tap re-fetch of the input is gone.  Both operands are
 // read with ds_read_b64_tr_b16 from tr_swz-swizzled images (patch rows = patch pixels, so the
 // B rows of tap (kh, kw) are the pixels (r + kh, c + kw)).  iters_per_split counts 256-row tiles.
-// Host guarantees (wgrad_variant_ok): igemm_patch_ok geometry, N % 64 == 0, no prologues.
+// Host guarantees (wgrad_variant_ok): igemm_patch_ok geometry, N % 64 == 0, no dY prologue;
+// PRO: the X operand's BN-apply + ReLU on the landed patch (256-row tiles inside one segment).
+template <bool PRO>
 __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
   constexpr int B = 64;  // co and ci tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1600,6 +1626,17 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // PRO: the [S<=2][sc, sh][64] table of this block's input-channel slice, staged in LDS behind
+  // the two stages BEFORE any DMA (global loads consumed inside the loop would make hipcc drain
+  // the in-flight opaque DMA with vmcnt(0); tools/isa_check.py)
+  float* Tb = (float*)(S0 + 2 * stage);
+  if (PRO) {
+    for (int i = tid; i < 2 * 2 * B; i += 576) {
+      const int sg = i / (2 * B), k = (i / B) & 1, j = i % B;
+      Tb[i] = sg < p.pro_S ? (k ? p.pro_sh : p.pro_sc)[sg * C + ci0 + j] : 0.f;
+    }
+    __syncthreads();
+  }
   const int kh = wid / 3, kw = wid - (wid / 3) * 3;
   const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
   typedef short i16x8 __attribute__((ext_vector_type(8)));
@@ -1609,6 +1646,32 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 < t_end) issue(t + 1, cur ^ 1);
+    if (PRO) {
+      // X operand = relu(bn(x)) of the conv's input, formed on the landed patch (the opaque
+      // DMA of tile t+1 into the other stage stays in flight); padding pixels stay zero
+      uint16_t* Pm = S0 + cur * stage + 256 * B;
+      const int img = (t * 256) / OHW;
+      const int row0 = (t * 256 - img * OHW) >> lg;
+      const int pseg = (t * 256) / p.pro_seg_rows;  // tiles never straddle a segment (host)
+      const float* psc = Tb + pseg * 2 * B;
+      const float* psh = psc + B;
+      for (int c = tid; c < PP * 8; c += 576) {
+        const int q = c >> 3, pc8 = c & 7;
+        const int pr = q / PW, pc = q - pr * PW;
+        const int ih = row0 - 1 + pr, iw = pc - 1;
+        if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
+          const int ch = tr_swz<B>(q, pc8 * 8);  // within the block's 64-channel slice
+          const float4 s0 = *(const float4*)(psc + ch), s1 = *(const float4*)(psc + ch + 4);
+          const float4 h0 = *(const float4*)(psh + ch), h1 = *(const float4*)(psh + ch + 4);
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+          u32x4* ptr = (u32x4*)(Pm + q * B + pc8 * 8);
+          *ptr = affine_relu8(*ptr, sc, sh, true, p.pro_relu != 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     const uint16_t* D = S0 + cur * stage;
     const uint16_t* P = D + 256 * B;
 #pragma unroll 2
@@ -1808,19 +1871,23 @@ size_t igemm_patch_lds(int BN, int NT, int OW, int C) {
   return std::max(patch, std::max(cst, red));
 }
 
-template <int BN, int WM, int WN, int EPI>
+template <int BN, int WM, int WN, int EPI, int PRO = 0>
 void launch_patch_t(const IgemmArgs& a0, hipStream_t s) {
   IgemmArgs a = a0;
   a.nMb = (a.M + 255) / 256;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
-  hipLaunchKernelGGL((igemm_patch<BN, WM, WN, EPI>), dim3(a.nMb * a.nNb), dim3(NT),
+  hipLaunchKernelGGL((igemm_patch<BN, WM, WN, EPI, PRO>), dim3(a.nMb * a.nNb), dim3(NT),
                      igemm_patch_lds(BN, NT, a.OW, a.C), s, a);
   HIP_CHECK_LAUNCH();
 }
 
 template <int BN, int WM, int WN>
 void launch_patch(const IgemmArgs& a, hipStream_t s) {
+  if (a.pro_sc != nullptr) {  // BN-apply prologue: the forward of a BN+ReLU-fed 3x3 conv
+    launch_patch_t<BN, WM, WN, 0, 1>(a, s);
+    return;
+  }
   switch (a.epi_mode) {
     case 1: launch_patch_t<BN, WM, WN, 1>(a, s); break;
     case 2: launch_patch_t<BN, WM, WN, 2>(a, s); break;
@@ -2022,10 +2089,13 @@ bool igemm_dual_ok(int v, const ConvGeom& g) {
   return lds <= 160 * 1024;
 }
 
+bool igemm_variant_is_patch(int v) { return v >= IG_PATCH0 && v < IG_GLDS8W; }
+
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
-  if (v >= IG_PATCH0 && v < IG_GLDS8W) return !pro && !bn_bwd_pro && igemm_patch_ok(g);
+  // patch kernel: BN-apply prologue (plain epilogue, host-checked) but no BN-backward one
+  if (v >= IG_PATCH0 && v < IG_GLDS8W) return !bn_bwd_pro && igemm_patch_ok(g);
   if (v >= IG_GLDS3 && v < IG_PATCH0 && (pro || bn_bwd_pro)) return false;
   if (bn_bwd_pro) {  // PRO 2 stages dY and x: doubled A staging + a 3 x C table must fit
     const int BM = IG_VARIANTS[v][0], BN = IG_VARIANTS[v][1];
@@ -2104,7 +2174,7 @@ int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
 bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < wgrad_num_variants(); }
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
-  if (v >= WG_PATCH0) return !pro && !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
+  if (v >= WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
   // wgrad_glds has the X-operand BN-apply prologue only (no dY BN-backward prologue)
   return v < WG_GLDS0 || (!dy_pro && igemm_glds_ok(g, pro, false));
 }
@@ -2169,8 +2239,12 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
       a.nCo = a.N / 64;
       a.nKk = a.C / 64;
       const int pp = (256 / a.OW + 2) * (a.OW + 2);
-      const size_t lds = (size_t)2 * (256 * 64 + (pp + 7) / 8 * 512) * 2;
-      hipLaunchKernelGGL(wgrad_patch, dim3(a.nCo * a.nKk * a.splits), dim3(576), lds, s, a);
+      const size_t lds = (size_t)2 * (256 * 64 + (pp + 7) / 8 * 512) * 2 +
+                         (a.pro_sc != nullptr ? (size_t)2 * 2 * 64 * 4 : 0);
+      if (a.pro_sc != nullptr)
+        hipLaunchKernelGGL(wgrad_patch<true>, dim3(a.nCo * a.nKk * a.splits), dim3(576), lds, s, a);
+      else
+        hipLaunchKernelGGL(wgrad_patch<false>, dim3(a.nCo * a.nKk * a.splits), dim3(576), lds, s, a);
       HIP_CHECK_LAUNCH();
       break;
     }

@@ -99,6 +99,7 @@ bool igemm_variant_glds(int v);  // LDS-DMA variant (see igemm_glds_ok)
 bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro);
 // can tile variant v run this geometry with these operand prologues (single source of truth for
 // the bindings' checks and the Python autotuner's candidate lists)
+bool igemm_variant_is_patch(int v);
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro);
 bool igemm_dual_ok(int v, const ConvGeom& g);  // block-output prologue (see igemm_glds)
 int igemm_block_m(int N);

@@ -143,6 +143,10 @@ class FusedStages:
         # mode — instead of zero-filling a full-resolution tensor (0.9 GB/step of fills at
         # ResNet-50 CIFAR) and re-reading it whole
         self.compact_ds = os.environ.get("SIMCLR_COMPACT_DS", "1") != "0"
+        # BN1-apply + ReLU of a bottleneck's 3x3 conv2 input in the patch kernels' prologue:
+        # off by default — the in-LDS pass over the halo'd patch costs more than the apply pass
+        # it saves (tools/patch_pro_bench.py: layer1 fwd +48 µs / wgrad +36 µs vs 42 µs apply)
+        self.patch_prologue = os.environ.get("SIMCLR_PATCH_PROLOGUE", "0") == "1"
         self._branch = None
         # a block's output (BN3 + shortcut + ReLU) formed inside the next block's conv1 prologue
         # instead of a separate pass that conv1 re-reads.  SIMCLR_BLOCK_OUT_PROLOGUE: 0 = off,
@@ -297,6 +301,16 @@ class FusedStages:
         igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl, tail=tail,
                      seg_rows=M // S if tail is not None else 0)
         return a, stats, M // bm // S, bs
+
+    def _patch_pro_ok(self, xn, cs: _ConvSpec) -> bool:
+        """3x3 / stride 1 / pad 1 conv at 16x16 or 32x32 with 64 / 128 input channels: the patch
+        kernels (forward igemm_patch, weight-gradient wgrad_patch) take the previous BatchNorm's
+        apply + ReLU in their prologue, so its output is never materialised."""
+        if not (getattr(self, "patch_prologue", False) and xn.is_cuda):
+            return False
+        Nb, H, W, C = xn.shape
+        return (cs.k == 3 and cs.stride == 1 and cs.pad == 1 and H == W and H in (16, 32)
+                and C in (64, 128))
 
     def _dual_ok(self, ops, xn, cs: _ConvSpec, S: int) -> bool:
         """Can ``cs`` (a block's conv1) form its input — the previous block's output — in its
@@ -723,9 +737,10 @@ class FusedStages:
                 forked = True
             for ci_, cs in enumerate(b.convs):
                 _ext.TAG = f"{b.name} conv{ci_ + 1} fwd"
-                if pro_ss is not None and cs.k > 1:
+                if pro_ss is not None and cs.k > 1 and not self._patch_pro_ok(cur, cs):
                     # a k x k conv re-gathers every input pixel k² times: applying BN+ReLU in
-                    # its prologue costs more VALU work than one materialising pass (measured)
+                    # its prologue costs more VALU work than one materialising pass (measured);
+                    # the LDS-resident patch kernels apply it once per patch pixel instead
                     bmat = torch.empty_like(cur)
                     ops.bn_apply_ss(cur, pro_ss, None, None, bmat, S, True)
                     cur, pro_ss = bmat, None

@@ -387,3 +387,50 @@ def test_bn_backward_prologue_every_variant(ops, N, H, Ci, Co):
         assert _rel(out, ref) < 1e-2, v
         seen_glds |= ops.igemm_variant_glds(v)
     assert seen_glds, "no LDS-DMA variant admitted the BN-backward prologue"
+
+
+@pytest.mark.parametrize("H,C,Co", [(32, 64, 64), (16, 128, 128)])
+def test_patch_kernels_bn_apply_prologue(ops, H, C, Co):
+    """The 3x3 patch kernels with the previous BatchNorm's apply + ReLU in their prologue
+    (forward igemm_patch PRO 1, weight-gradient wgrad_patch PRO) == materialising
+    relu(x·sc + sh) with bn_apply_ss first — every admissible variant, padding kept zero."""
+    from simclr_amd.ops.conv_hip import fwd_geom
+    torch.manual_seed(13)
+    N, S = 8, 2
+    M = N * H * H
+    x = _bf(torch.randn(N, H, H, C, device=DEV))
+    sc = torch.rand(S, C, device=DEV) + 0.5
+    sh = torch.randn(S, C, device=DEV) * 0.5  # shifts > 0 would leak into a non-zero padding
+    ss = torch.stack([sc, sh]).reshape(2, S * C).contiguous()
+    xb = torch.empty_like(x)
+    ops.bn_apply_ss(x, ss, None, None, xb, S, True)
+    w = _bf(torch.randn(Co, 3, 3, C, device=DEV) / math.sqrt(9 * C)).contiguous()
+    g = fwd_geom(N, H, H, C, H, H, 3, 3, 1, 1, Co)
+    ref = torch.empty(N, H, H, Co, device=DEV, dtype=torch.bfloat16)
+    ops.igemm(xb, w, ref, None, None, g, None, None, 0, False, 0, None, None, 15 if Co == 64 else 16)
+    patch_seen = False
+    for v in range(ops.igemm_nvariants()):
+        if not ops.igemm_variant_ok(v, g, True, False) or (M // S) % ops.igemm_variant_bm(v):
+            continue
+        out = torch.empty_like(ref)
+        ops.igemm(x, w, out, None, None, g, ss[0], ss[1], M // S, True, 0, None, None, v)
+        assert _rel(out, ref) < 1e-2, v
+        patch_seen |= ops.igemm_variant_glds(v)  # the only LDS-DMA kernel admitting a padded pro
+    assert patch_seen
+    dy = _bf(torch.randn(N, H, H, Co, device=DEV))
+    outs = {}
+    for v in range(ops.wgrad_nvariants()):
+        if not ops.wgrad_variant_ok(v, g, True, False):
+            continue
+        sp = ops.wgrad_splits(g, v)
+        part = torch.empty(sp * Co * 9 * C, device=DEV)
+        o = torch.empty(Co, 3, 3, C, device=DEV)
+        ops.wgrad(dy, x, part, o, g, sp, C, 0.0, ss[0], ss[1], M // S, True, S, v)
+        outs[v] = o
+    sp = ops.wgrad_splits(g, 17)
+    part = torch.empty(sp * Co * 9 * C, device=DEV)
+    wref = torch.empty(Co, 3, 3, C, device=DEV)
+    ops.wgrad(dy, xb, part, wref, g, sp, C, 0.0, None, None, 0, False, 1, 17)
+    assert 17 in outs, "wgrad_patch did not admit the X prologue"
+    for v, o in outs.items():
+        assert _rel(o, wref) < 1e-2, v
