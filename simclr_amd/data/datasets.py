@@ -84,9 +84,12 @@ def _cifar_bin(root: Path, name: str, train: bool) -> Optional[ImageDataset]:
 
 
 def synthetic_dataset(n: int, num_classes: int = 10, size: int = 32, seed: int = 0,
-                      name: str = "synthetic", template_seed: int = 1234) -> ImageDataset:
+                      name: str = "synthetic", template_seed: int = 1234, noise: float = 25.0,
+                      colour: bool = True) -> ImageDataset:
     """Class-structured random images: per-class colour/frequency template + per-image noise,
-    so that learned features are non-trivially separable (used when no data is on disk)."""
+    so that learned features are non-trivially separable (used when no data is on disk).
+    ``colour=False`` gives every class the same mean colour (texture is the only cue) and a
+    larger ``noise`` makes the task harder (tools/e2e_probe.sh)."""
     g = np.random.default_rng(seed)
     labels = g.integers(0, num_classes, size=n).astype(np.int64)
     yy, xx = np.meshgrid(np.linspace(0, 1, size), np.linspace(0, 1, size), indexing="ij")
@@ -94,6 +97,8 @@ def synthetic_dataset(n: int, num_classes: int = 10, size: int = 32, seed: int =
     cg = np.random.default_rng(template_seed)  # shared by train and test splits
     for c in range(num_classes):
         col = cg.uniform(40, 215, size=3)
+        if not colour:
+            col = np.full(3, 128.0)
         fy, fx = cg.uniform(1, 4, size=2)
         ph = cg.uniform(0, 2 * np.pi)
         pat = np.sin(2 * np.pi * (fy * yy + fx * xx) + ph)
@@ -102,15 +107,16 @@ def synthetic_dataset(n: int, num_classes: int = 10, size: int = 32, seed: int =
     bs = 4096
     for s in range(0, n, bs):
         e = min(n, s + bs)
-        noise = g.normal(0, 25.0, size=(e - s, size, size, 3)).astype(np.float32)
-        imgs[s:e] = np.clip(tmpl[labels[s:e]] + noise, 0, 255).astype(np.uint8)
+        eps = g.normal(0, noise, size=(e - s, size, size, 3)).astype(np.float32)
+        imgs[s:e] = np.clip(tmpl[labels[s:e]] + eps, 0, 255).astype(np.uint8)
     return ImageDataset(imgs, labels, num_classes, name, synthetic=True)
 
 
 def load_dataset(name: str, train: bool = True, root: str = DEFAULT_ROOT,
                  synthetic: bool = False, synthetic_size: Optional[int] = None,
                  allow_synthetic_fallback: bool = False, seed: int = 0,
-                 image_size: int = 32) -> ImageDataset:
+                 image_size: int = 32, synthetic_noise: float = 25.0,
+                 synthetic_colour: bool = True) -> ImageDataset:
     name = name.lower()
     if name not in ("cifar10", "cifar100"):
         raise ValueError("experiment.name must be cifar10 or cifar100, got {!r}".format(name))
@@ -127,4 +133,5 @@ def load_dataset(name: str, train: bool = True, root: str = DEFAULT_ROOT,
                 "place the CIFAR python/binary batches there or run with data.synthetic=true")
     n = synthetic_size if synthetic_size is not None else (50000 if train else 10000)
     return synthetic_dataset(n, ncls, size=image_size, seed=seed + (0 if train else 7919),
-                             name=f"synthetic-{name}")
+                             name=f"synthetic-{name}", noise=synthetic_noise,
+                             colour=synthetic_colour)

@@ -76,6 +76,8 @@ def _datasets(cfg):
     kw = dict(root=cfg_get(cfg, "data.root", "~/pytorch_datasets"),
               synthetic=bool(cfg_get(cfg, "data.synthetic", False)),
               allow_synthetic_fallback=bool(cfg_get(cfg, "data.synthetic_fallback", False)),
+              synthetic_noise=float(cfg_get(cfg, "data.synthetic_noise", 25.0)),
+              synthetic_colour=bool(cfg_get(cfg, "data.synthetic_colour", True)),
               seed=seed)
     size = cfg_get(cfg, "data.synthetic_size", None)
     tr = load_dataset(cfg["experiment"]["name"], train=True,

@@ -164,6 +164,8 @@ def pretrain(cfg) -> dict:
                       root=cfg_get(cfg, "data.root", "~/pytorch_datasets"),
                       synthetic=bool(cfg_get(cfg, "data.synthetic", False)),
                       synthetic_size=cfg_get(cfg, "data.synthetic_size", None),
+                      synthetic_noise=float(cfg_get(cfg, "data.synthetic_noise", 25.0)),
+                      synthetic_colour=bool(cfg_get(cfg, "data.synthetic_colour", True)),
                       allow_synthetic_fallback=bool(cfg_get(cfg, "data.synthetic_fallback", False)),
                       seed=seed)
     loader = ContrastiveLoader(ds, cfg["experiment"]["batches"], st.device, rank=rank,
