@@ -10,6 +10,7 @@ normalises away the (dominant) common component of h, so z — and every gradien
 bf16-noise-dominated and differs by tens of percent between ANY two reduction orders (measured:
 tools/debug_dist.py shows per-layer batch statistics agreeing to 1e-4..1e-3 while z differs by
 ~30%).  The head's distributed semantics are covered by the fp32 CPU test."""
+import math
 import os
 import socket
 
@@ -187,3 +188,33 @@ def test_two_ranks_match_one_process(tmp_path, fused, ipc):
     assert dist_g <= 3 * noise_g + 2e-3, msg
     assert dist_bn <= 3 * noise_bn + 2e-3, msg
     assert dist_rs <= 3 * noise_rs + 2e-3, msg
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("bn_comm", ["rccl", "ipc"])
+def test_bench_two_ranks_one_gpu(tmp_path, bn_comm):
+    """The driver's N>1 bench flow (torch.distributed.run, one process per rank, max over ranks,
+    rank 0 prints one JSON line) rehearsed with 2 ranks on this box's one GPU over gloo (RCCL
+    refuses two ranks on one device): global negatives, the bucketed gradient all-reduce, the
+    BatchNorm statistics over the process group or the IPC arenas, the IPC timeout guard."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, SIMCLR_DIST_BACKEND="gloo", SIMCLR_BN_COMM=bn_comm,
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(root / "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "64"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=540)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["value"] > 0 and j["config"]["parallelism"] == "dp2"
+    assert j["config"]["global_batch"] == 128
+    assert "global-negatives" in j["config"]["loss"], j["config"]["loss"]
+    assert j["config"]["bn_stats_comm"] == bn_comm, j["config"]
+    assert math.isfinite(j["config"]["final_loss"])
