@@ -280,8 +280,27 @@ __global__ void k_reduce_loss(const float* __restrict__ loss, int R, float scale
   }
 }
 
-int splits_for(int tiles, int ptiles) {
-  int s = (512 + tiles - 1) / tiles;
+// One-wave blocks, latency-bound on their L2 operand loads: each block should walk about 8
+// partner tiles (128 columns), with at least 512 blocks (so the SIMDs have waves to switch
+// between) and at most 4096 (the split partials grow with the count).  tools/ntxent_bench.py,
+// R = 1024: at 8192 global negatives (8 ranks) the fixed 512-block rule took 85 + 107 + 327 µs
+// (forward, column and row gradient passes), this one ~57 + 78 + 94; at 1024 columns it keeps
+// 512.  SIMCLR_NTX_BLOCKS=N forces a fixed block target (experiments).
+int ntx_fixed_blocks() {
+  static const int t = [] {
+    const char* e = getenv("SIMCLR_NTX_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  return t;
+}
+
+int splits_for(int tiles, int ptiles, int tiles_per_block = 8) {
+  long target = ntx_fixed_blocks();
+  if (target <= 0) {
+    target = (long)tiles * ptiles / tiles_per_block;
+    target = target < 512 ? 512 : (target > 4096 ? 4096 : target);
+  }
+  int s = (int)((target + tiles - 1) / tiles);
   if (s > ptiles) s = ptiles;
   if (s < 1) s = 1;
   return s;
@@ -302,8 +321,12 @@ void ntxent_transpose(const float* in, float* out, int R, int D, hipStream_t s) 
   HIP_CHECK_LAUNCH();
 }
 
-int ntxent_fwd_splits(int R, int Ccols) { return splits_for(R / 16, Ccols / 16); }
-int ntxent_bwd_splits(int nown, int npart) { return splits_for(nown / 16, npart / 16); }
+// measured optimum (tools/ntxent_bench.py, 8192 columns): ~16 partner tiles per block for the
+// forward (57 µs vs 74 at 8) and the column pass (73 vs 78), ~8 for the row pass (93 vs 110)
+int ntxent_fwd_splits(int R, int Ccols) { return splits_for(R / 16, Ccols / 16, 16); }
+int ntxent_bwd_splits(int nown, int npart) {
+  return splits_for(nown / 16, npart / 16, nown <= npart ? 8 : 16);
+}
 
 void ntxent_forward(const float* znT, int R, int Ccols, int D, int col_offset, int n_local,
                     float inv_temp, float* part, int splits, float* lse, float* loss,
