@@ -239,8 +239,6 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   ConvFusion f = fusion_from(pro_sc, pro_sh, pro_seg_rows, pro_relu, 1, epi_mode, epi_a, epi_b,
                              g.C, epi_sub ? sub_numel : out.numel());
   f.epi_a_sub = epi_sub ? 1 : 0;
-  TORCH_CHECK(!(f.pro_sc && igemm_variant_is_patch((int)variant) && epi_mode != 0),
-              "igemm: the patch kernel's BN-apply prologue runs with the plain epilogue only");
   if (epi_sub && epi_mode == 2)
     TORCH_CHECK(epi_b->numel() >= out.numel(), "epilogue operand b");
   f.seg_rows = (int)seg_rows;

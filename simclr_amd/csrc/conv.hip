@@ -201,7 +201,7 @@ __device__ __forceinline__ void epi_load_batch(const IgemmArgs& p, int m0, int n
 // the HBM-heaviest epilogue) load their first row batch before the main loop, so its latency
 // overlaps the operand DMA of the (short-K) GEMM instead of following it.
 template <int EPI>
-constexpr bool epi_prefetch() { return EPI == 4 || EPI == 5; }
+constexpr bool epi_prefetch() { return EPI == 3 || EPI == 4 || EPI == 5; }
 
 // BatchNorm finalize in the last blocks of the launch (bn_tail.h): the last of every level-1
 // group of `gr` row-blocks (same segment, same channel tile) sums the group's partial rows; the
@@ -996,8 +996,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
 // patch at shifted pixel positions; only the weight tile streams per k-step (2 LDS stages).
 // Patch image: [pixel][C] with 16-byte chunk c of pixel q stored at chunk c ^ (q & 7).
 // Host guarantees (igemm_variant_ok): KH = KW = 3, unit strides, ih0 = iw0 = -1, OH = IH,
-// OW = IW in {16, 32}, C in {64, 128}, direct output; PRO 1 (BN-apply + ReLU on the landed
-// patch, padding kept zero) only with the plain epilogue.
+// OW = IW in {16, 32}, C in {64, 128}, direct output; PRO 1: BN-apply + ReLU on the landed
+// patch, padding kept zero.
 template <int BN, int WM, int WN, int EPI, int PRO>
 __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
   constexpr int BM = 256;
@@ -1884,8 +1884,19 @@ void launch_patch_t(const IgemmArgs& a0, hipStream_t s) {
 
 template <int BN, int WM, int WN>
 void launch_patch(const IgemmArgs& a, hipStream_t s) {
-  if (a.pro_sc != nullptr) {  // BN-apply prologue: the forward of a BN+ReLU-fed 3x3 conv
-    launch_patch_t<BN, WM, WN, 0, 1>(a, s);
+  if (a.pro_sc != nullptr) {  // BN-apply prologue on the landed patch, any epilogue
+    switch (a.epi_mode) {
+      case 1: launch_patch_t<BN, WM, WN, 1, 1>(a, s); break;
+      case 2: launch_patch_t<BN, WM, WN, 2, 1>(a, s); break;
+      case 3: launch_patch_t<BN, WM, WN, 3, 1>(a, s); break;
+      case 4:
+        if (a.stats2 != nullptr)
+          launch_patch_t<BN, WM, WN, 5, 1>(a, s);
+        else
+          launch_patch_t<BN, WM, WN, 4, 1>(a, s);
+        break;
+      default: launch_patch_t<BN, WM, WN, 0, 1>(a, s); break;
+    }
     return;
   }
   switch (a.epi_mode) {
@@ -2094,7 +2105,7 @@ bool igemm_variant_is_patch(int v) { return v >= IG_PATCH0 && v < IG_GLDS8W; }
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
-  // patch kernel: BN-apply prologue (plain epilogue, host-checked) but no BN-backward one
+  // patch kernel: BN-apply prologue but no BN-backward one
   if (v >= IG_PATCH0 && v < IG_GLDS8W) return !bn_bwd_pro && igemm_patch_ok(g);
   if (v >= IG_GLDS3 && v < IG_PATCH0 && (pro || bn_bwd_pro)) return false;
   if (bn_bwd_pro) {  // PRO 2 stages dY and x: doubled A staging + a 3 x C table must fit
