@@ -747,6 +747,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // DMA instructions per wave per tile
   static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "glds tiling");
+  // WN == 1 tiles: every wave owns its A rows, so PRO 1 transforms the A fragments in registers
+  // after the ds_read (each element exactly once) instead of a read-modify-write pass over the
+  // landed tile plus a barrier per k-tile
+  constexpr bool RPRO = PRO == 1 && WN == 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int stages = p.K > 64 ? NST : 1;
   constexpr int NA = PRO >= 2 ? 2 : 1;  // PRO 2 / 3 stage a second A-shaped operand (Rs)
@@ -775,7 +779,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   const int lrow = lane >> 3, pch = lane & 7;
   const int lch = pch ^ lrow;
   const int OHW = p.OH * p.OW;
-  int a_pix[AI], a_ih[AI], a_iw[AI];
+  // Issue cost: every DMA address below is one add on per-thread values fixed for the whole
+  // block, plus wave-uniform (scalar) per-k-tile terms.  The tap / channel walk of the k-tiles is
+  // carried incrementally in scalar registers (a runtime integer division lowers to a VALU
+  // reciprocal sequence even for uniform operands), the row's tap-(0, 0) offset is computed
+  // once, and the LDS destinations come from the scalar wave index — the first cut spent ~40
+  // VALU instructions (two quarter-rate multiplies) per DMA, comparable to the k-tile's MFMA time.
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  int a_base[AI], a_ih[AI], a_iw[AI];
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
     const int m = m0 + (j * NW + wid) * 8 + lrow;
@@ -785,9 +796,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     const int rem = mm - n * OHW;
     const int oh = rem / p.OW;
     const int ow = rem - oh * p.OW;
-    a_pix[j] = n * p.IH * p.IW;
-    a_ih[j] = ok ? oh * p.ish + p.ih0 : -(1 << 28);  // invalid rows fail the bounds test
-    a_iw[j] = ow * p.isw + p.iw0;
+    const int ih = oh * p.ish + p.ih0, iw = ow * p.isw + p.iw0;
+    // tap-(0, 0) byte offset of the lane's chunk: may lie outside the tensor for padded taps,
+    // used only when the bounds test passes (int32: a_bytes < 2^31 host-checked)
+    a_base[j] = ((n * p.IH + ih) * p.IW + iw) * p.C * 2 + lch * 16;
+    a_ih[j] = ok ? ih : -(1 << 28);  // invalid rows fail the bounds test
+    a_iw[j] = iw;
   }
   uint32_t b_off[BI];
 #pragma unroll
@@ -796,36 +810,41 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     b_off[j] = nrow < p.N ? (uint32_t)(nrow * p.K + lch * 8) * 2u : p.b_bytes;
   }
   const uint32_t OOB_A = p.a_bytes;
+  int nx_c = 0, nx_kh = 0, nx_kw = 0;  // channel offset and tap of the next k-tile to issue
 
-  auto issue = [&](int kt, int buf) {
-    const int k0 = kt * 64;
-    const int tap = k0 / p.C;  // wave-uniform
-    const int ci = k0 - tap * p.C + lch * 8;
-    const int kh = tap / p.KW;
-    const int kw = tap - kh * p.KW;
-    const int dih = kh * p.dh, diw = kw * p.dw;
+  auto issue = [&](int kt, int buf) {  // called for kt = 0, 1, 2, ... in order
+    const int dih = nx_kh * p.dh, diw = nx_kw * p.dw;
+    const int delta = ((dih * p.IW + diw) * p.C + nx_c) * 2;
+    nx_c += 64;
+    if (nx_c == p.C) {
+      nx_c = 0;
+      if (++nx_kw == p.KW) { nx_kw = 0; ++nx_kh; }
+    }
+    uint16_t* Aw = As + buf * BM * 64 + wid_u * 8 * 64;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
       const int ih = a_ih[j] + dih;
       const int iw = a_iw[j] + diw;
       const bool ok = (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-      const uint32_t off =
-          ok ? (uint32_t)(((a_pix[j] + ih * p.IW + iw) * p.C + ci) * 2) : OOB_A;
+      const uint32_t off = ok ? (uint32_t)(a_base[j] + delta) : OOB_A;
       // the prologues store into the landed tile: the builtin DMA would be drained right
       // after its issue (see dma16_opaque), so those kernels issue it opaquely
       if (PRO) {
-        dma16_opaque(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
-        if (PRO >= 2) dma16_opaque(rr, Rs + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+        dma16_opaque(ra, Aw + j * NW * 8 * 64, off);
+        if (PRO >= 2)
+          dma16_opaque(rr, Rs + buf * BM * 64 + wid_u * 8 * 64 + j * NW * 8 * 64, off);
       } else {
-        dma16(ra, As + buf * BM * 64 + (j * NW + wid) * 8 * 64, off);
+        dma16(ra, Aw + j * NW * 8 * 64, off);
       }
     }
+    uint16_t* Bw = Bs + buf * BN * 64 + wid_u * 8 * 64;
+    const uint32_t kb = (uint32_t)kt * 128u;
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
       if (PRO)
-        dma16_opaque(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)k0 * 2u);
+        dma16_opaque(rb, Bw + j * NW * 8 * 64, b_off[j] + kb);
       else
-        dma16(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)k0 * 2u);
+        dma16(rb, Bw + j * NW * 8 * 64, b_off[j] + kb);
     }
   };
 
@@ -873,23 +892,31 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     // wave, every wave done reading the buffer the next issue overwrites
     __builtin_amdgcn_s_barrier();
     if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    // prologue passes over the landed tile: chunk c = tid + i·NT sits in row c / 8 and holds
+    // logical channel chunk (c % 8) ^ (row % 8), the same for every i (NT % 64 == 0), so the
+    // per-channel tables are read from LDS once per k-tile rather than once per chunk (LDS
+    // stores into the tile keep hipcc from hoisting them itself), and every chunk of the thread
+    // is loaded before the first is written back
+    constexpr int PCH = BM * 8 / NT;  // chunks per thread
+    static_assert(NT % 64 == 0, "prologue chunk mapping");
+    const int plc = (tid & 7) ^ ((tid >> 3) & 7);
     if (PRO == 3) {
-      const int ci0 = kt * 64;  // 1x1: K = C
+      const int ci = kt * 64 + plc * 8;  // 1x1: K = C
+      float tb[4][8];  // sc, sh, rsc, rsh of the thread's 8 channels
 #pragma unroll
-      for (int i = 0; i < BM * 8 / NT; ++i) {
+      for (int t = 0; t < 4; ++t) {
+        const float4* pt = (const float4*)(Pt + t * p.C + ci);
+        const float4 t0 = pt[0], t1 = pt[1];
+        tb[t][0] = t0.x; tb[t][1] = t0.y; tb[t][2] = t0.z; tb[t][3] = t0.w;
+        tb[t][4] = t1.x; tb[t][5] = t1.y; tb[t][6] = t1.z; tb[t][7] = t1.w;
+      }
+      // (one chunk at a time here: the 8-wave 256 x 256 tile has no registers to spare)
+#pragma unroll
+      for (int i = 0; i < PCH; ++i) {
         const int c = tid + i * NT;
-        const int row = c >> 3, lc = (c & 7) ^ (row & 7);
-        const int ci = ci0 + lc * 8;
-        u32x4* q = (u32x4*)(As + cur * BM * 64 + c * 8);
-        const u32x4 v = *q, r = *(const u32x4*)(Rs + cur * BM * 64 + c * 8);
-        float tb[4][8];  // sc, sh, rsc, rsh of the chunk's 8 channels (ds_read_b128 x 8)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const float4* pt = (const float4*)(Pt + t * p.C + ci);
-          const float4 t0 = pt[0], t1 = pt[1];
-          tb[t][0] = t0.x; tb[t][1] = t0.y; tb[t][2] = t0.z; tb[t][3] = t0.w;
-          tb[t][4] = t1.x; tb[t][5] = t1.y; tb[t][6] = t1.z; tb[t][7] = t1.w;
-        }
+        const int row = c >> 3;
+        const u32x4 v = *(const u32x4*)(As + cur * BM * 64 + c * 8);
+        const u32x4 r = *(const u32x4*)(Rs + cur * BM * 64 + c * 8);
         float o[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -902,7 +929,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
         u32x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = pack2bf(o[2 * e], o[2 * e + 1]);
-        *q = w;
+        *(u32x4*)(As + cur * BM * 64 + c * 8) = w;
         if (nb == 0) {  // block-uniform: every wave issues the same 2 stores per chunk
           const size_t o8 = (size_t)(m0 + row) * p.C + ci;
           __builtin_nontemporal_store(w, (u32x4*)(p.pro_out + o8));
@@ -918,40 +945,42 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       // BatchNorm backward of the layer this conv's dgrad consumes, on the landed tiles: the
       // DMA brought dY (As) and the pre-BN activation (Rs); the GEMM operand is
       // A·dY + B·x + D (1x1 unpadded only: no padding taps, K = C)
-      const int ci0 = kt * 64;
+      const int ci = kt * 64 + plc * 8;
+      float tb[3][8];
 #pragma unroll
-      for (int i = 0; i < BM * 8 / NT; ++i) {
-        const int c = tid + i * NT;
-        const int row = c >> 3, lc = (c & 7) ^ (row & 7);
-        const int ci = ci0 + lc * 8;
-        u32x4* q = (u32x4*)(As + cur * BM * 64 + c * 8);
-        const u32x4 r = *(const u32x4*)(Rs + cur * BM * 64 + c * 8);
-        float tb[3][8];
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const float4* pt = (const float4*)(Pt + t * p.C + ci);
-          const float4 t0 = pt[0], t1 = pt[1];
-          tb[t][0] = t0.x; tb[t][1] = t0.y; tb[t][2] = t0.z; tb[t][3] = t0.w;
-          tb[t][4] = t1.x; tb[t][5] = t1.y; tb[t][6] = t1.z; tb[t][7] = t1.w;
-        }
-        *q = bnbwd8(*q, r, tb[0], tb[1], tb[2], true);
+      for (int t = 0; t < 3; ++t) {
+        const float4* pt = (const float4*)(Pt + t * p.C + ci);
+        const float4 t0 = pt[0], t1 = pt[1];
+        tb[t][0] = t0.x; tb[t][1] = t0.y; tb[t][2] = t0.z; tb[t][3] = t0.w;
+        tb[t][4] = t1.x; tb[t][5] = t1.y; tb[t][6] = t1.z; tb[t][7] = t1.w;
       }
+      u32x4 va[PCH], vr[PCH];
+#pragma unroll
+      for (int i = 0; i < PCH; ++i) {
+        const int c = tid + i * NT;
+        va[i] = *(const u32x4*)(As + cur * BM * 64 + c * 8);
+        vr[i] = *(const u32x4*)(Rs + cur * BM * 64 + c * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < PCH; ++i)
+        *(u32x4*)(As + cur * BM * 64 + (tid + i * NT) * 8) =
+            bnbwd8(va[i], vr[i], tb[0], tb[1], tb[2], true);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-    } else if (PRO) {
-      const int ci0 = kt * 64 - (kt * 64 / p.C) * p.C;
+    } else if (PRO && !RPRO) {
+      const int ci = kt * 64 + plc * 8;  // 1x1 (host-checked): K = C
+      const float4* ps = (const float4*)(Pt + ci);
+      const float4* ph = (const float4*)(Pt + p.C + ci);
+      const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      u32x4 va[PCH];
 #pragma unroll
-      for (int i = 0; i < BM * 8 / NT; ++i) {
-        const int c = tid + i * NT;
-        const int row = c >> 3, lc = (c & 7) ^ (row & 7);
-        const float4* ps = (const float4*)(Pt + ci0 + lc * 8);
-        const float4* ph = (const float4*)(Pt + p.C + ci0 + lc * 8);
-        const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
-        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-        u32x4* q = (u32x4*)(As + cur * BM * 64 + c * 8);
-        *q = affine_relu8(*q, sc, sh, true, p.pro_relu != 0);
-      }
+      for (int i = 0; i < PCH; ++i) va[i] = *(const u32x4*)(As + cur * BM * 64 + (tid + i * NT) * 8);
+#pragma unroll
+      for (int i = 0; i < PCH; ++i)
+        *(u32x4*)(As + cur * BM * 64 + (tid + i * NT) * 8) =
+            affine_relu8(va[i], sc, sh, true, p.pro_relu != 0);
       // raw barrier: __syncthreads() would also drain the next tile's DMA (vmcnt(0))
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -966,6 +995,20 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
         const int row = wm * TM + fm * 16 + (lane & 15);
         const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
         af[fm] = *(const bf16x8*)(Ab + row * 64 + ch * 8);
+      }
+      if constexpr (RPRO) {
+        // the lane's 8 channels (logical chunk ks*4 + lane/16 of this k-tile) are the same for
+        // every fragment row: one table read per k-half, the transform on the A fragments
+        const int ci = kt * 64 + (ks * 4 + (lane >> 4)) * 8;  // 1x1 (host-checked): K = C
+        const float4* ps = (const float4*)(Pt + ci);
+        const float4* ph = (const float4*)(Pt + p.C + ci);
+        const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          af[fm] = __builtin_bit_cast(
+              bf16x8, affine_relu8(__builtin_bit_cast(u32x4, af[fm]), sc, sh, true, p.pro_relu != 0));
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
@@ -2042,11 +2085,13 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
                                   {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256},
                                   {256, 128}, {128, 128}, {128, 256},
                                   {256, 64}, {256, 128},
-                                  {256, 64}};
+                                  {256, 64}, {128, 256}, {256, 128}};
 constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
 constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
 constexpr int IG_PATCH0 = 15;  // 3x3 stride-1 kernel with an LDS-resident input patch
 constexpr int IG_GLDS8W = 17;  // 2-stage LDS-DMA, 256 x 64 tile on 8 waves (memory-bound 1x1)
+// 18, 19: 2-stage LDS-DMA, one wave column (WN = 1): the BN-apply prologue runs on the A
+// fragments in registers (the short-K 1x1 expansion convs, conv3 of a bottleneck)
 // variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
 // {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
 // that many blocks; every split costs an fp32 N x K slab written here and re-read by the
@@ -2088,7 +2133,7 @@ bool igemm_patch_ok(const ConvGeom& g) {
 // block-output prologue (PRO 3): 2-stage LDS-DMA tiles whose doubled A staging fits the LDS,
 // on 1x1 / stride-1 / unpadded / direct-output convolutions (A row m = output row m)
 bool igemm_dual_ok(int v, const ConvGeom& g) {
-  if (!((v >= IG_GLDS0 && v < IG_GLDS3) || v == IG_GLDS8W) || !igemm_glds_ok(g, true, false))
+  if (!((v >= IG_GLDS0 && v < IG_GLDS3) || v >= IG_GLDS8W) || !igemm_glds_ok(g, true, false))
     return false;
   const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
                       g.OWp == g.OW;
@@ -2162,6 +2207,8 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 15: launch_patch<64, 4, 1>(a, s); break;
     case 16: launch_patch<128, 4, 2>(a, s); break;
     case 17: launch_glds<256, 64, 8, 1>(a, s); break;
+    case 18: launch_glds<128, 256, 4, 1>(a, s); break;
+    case 19: launch_glds<256, 128, 8, 1>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
