@@ -1569,6 +1569,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
     }
     __syncthreads();
   }
+  constexpr int PXC = 64 * CPX / (64 * NW);  // X-prologue chunks per thread per step
+  // the thread's chunks share their tr_swz key (row bits 0-3) when they are 16k rows apart;
+  // the 32 table registers only where the accumulators leave room (256 x 256: 128 of them)
+  constexpr bool HOIST = (64 * NW / CPX) % 16 == 0 && (BCO / WM / 16) * (BKK / WN / 16) * 4 <= 64;
+  const int ptc = tid % CPX;                             // the thread's physical chunk
+  float pro_sc0[8], pro_sh0[8], pro_sc1[8], pro_sh1[8];  // its logical column's tables
+  if (PRO && HOIST) {
+    const int col = tr_swz<BKK>(tid / CPX, ptc * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pro_sc0[e] = Pt[col + e];
+      pro_sc1[e] = Pt[BKK + col + e];
+      pro_sh0[e] = Pt[2 * BKK + col + e];
+      pro_sh1[e] = Pt[3 * BKK + col + e];
+    }
+  }
   if (nit > 0) issue(0, 0);
   if (NST == 3 && nit > 1) issue(1, 1);
   for (int it = 0; it < nit; ++it) {
@@ -1580,12 +1596,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // step it landed for every wave; buffer (it-1) % NST is free
     if (it + NST - 1 < nit) issue(it + NST - 1, (it + NST - 1) % NST);
-    if (PRO) {
+    if (PRO && !HOIST) {
       // rows past mend hold zero dY, so whatever the transform makes of them contributes 0;
       // columns past K are dropped by the store
       const int mb = mbeg + it * 64;
 #pragma unroll
-      for (int i = 0; i < 64 * CPX / (64 * NW); ++i) {
+      for (int i = 0; i < PXC; ++i) {
         const int c = tid + i * 64 * NW;
         const int row = c / CPX, pc = c % CPX;
         const int col = tr_swz<BKK>(row, pc * 8);
@@ -1597,6 +1613,37 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
         const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
         u32x4* q = (u32x4*)(Xs + cur * 64 * BKK + row * BKK + pc * 8);
         *q = affine_relu8(*q, sc, sh, true, p.pro_relu != 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else if (PRO) {
+      // as above; here the thread's chunks sit in rows a multiple of
+      // 16 apart, so they share one logical column (tr_swz keys on row bits 0-3) and the same
+      // rows recur every step: the tables were loaded into registers once (pro_sc0 .. pro_sh1),
+      // and a step that lies inside one segment picks its set with a uniform branch
+      const int mb = mbeg + it * 64;
+      const bool seg1 = p.pro_S > 1 && mb >= p.pro_seg_rows;
+      const bool mixed = p.pro_S > 1 && mb < p.pro_seg_rows && mb + 64 > p.pro_seg_rows;
+      const bool relu = p.pro_relu != 0;
+#pragma unroll
+      for (int i = 0; i < PXC; ++i) {
+        const int row = (tid + i * 64 * NW) / CPX;
+        u32x4* q = (u32x4*)(Xs + cur * 64 * BKK + row * BKK + ptc * 8);
+        const u32x4 v = *q;
+        if (mixed) {
+          const bool sg = mb + row >= p.pro_seg_rows;
+          float sc[8], sh[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            sc[e] = sg ? pro_sc1[e] : pro_sc0[e];
+            sh[e] = sg ? pro_sh1[e] : pro_sh0[e];
+          }
+          *q = affine_relu8(v, sc, sh, true, relu);
+        } else if (seg1) {
+          *q = affine_relu8(v, pro_sc1, pro_sh1, true, relu);
+        } else {
+          *q = affine_relu8(v, pro_sc0, pro_sh0, true, relu);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
