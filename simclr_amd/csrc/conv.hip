@@ -105,6 +105,26 @@ __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const fl
   return w;
 }
 
+// Packed form of affine_relu8 for the register-side prologue (no out-of-range lanes): two
+// channels per v_pk_fma_f32, one v_cvt_pk_bf16_f32, and the ReLU as a packed signed 16-bit max
+// on the bf16 bit patterns (a negative bf16 is a negative int16; -0 becomes +0)
+__device__ __forceinline__ u32x4 affine_relu8_pk(u32x4 v, const f32x2* sc, const f32x2* sh,
+                                                 bool relu) {
+  typedef short i16x2 __attribute__((ext_vector_type(2)));
+  u32x4 w;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const f32x2 x = {lo_bf(v[e]), hi_bf(v[e])};
+    const f32x2 y = __builtin_elementwise_fma(x, sc[e], sh[e]);
+    uint32_t q = pack2bf(y.x, y.y);
+    if (relu)
+      q = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, q),
+                                                                 (i16x2){0, 0}));
+    w[e] = q;
+  }
+  return w;
+}
+
 __device__ __forceinline__ u32x4 bnbwd8(u32x4 g, u32x4 x, const float* A, const float* B,
                                         const float* D, bool ok) {
   u32x4 w;
@@ -367,12 +387,19 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
   constexpr int NIT = BM / RSTEP;
   constexpr int UNR = epi_unr<BM, BN, NT>();
   static_assert(NIT % UNR == 0, "epilogue batches");
+  // software-pipelined: the next batch's operand loads are issued before this batch is
+  // processed and stored, so a block keeps two batches of streamed operands in flight (the
+  // residual-gradient modes read ~2x what they write; one batch at a time exposed a full
+  // memory latency per batch).  The accumulators are dead here (staged in Cs), so the second
+  // batch's registers are free.
+  EpiBatch<UNR> Bn;
+  if (pre != nullptr)
+    Bn = *pre;
+  else
+    epi_load_batch<BM, BN, NT, EPI>(p, m0, n0, 0, Bn);
   for (int it0 = 0; it0 < NIT; it0 += UNR) {
-    EpiBatch<UNR> B;
-    if (pre != nullptr && it0 == 0)
-      B = *pre;
-    else
-      epi_load_batch<BM, BN, NT, EPI>(p, m0, n0, it0, B);
+    const EpiBatch<UNR> B = Bn;
+    if (it0 + UNR < NIT) epi_load_batch<BM, BN, NT, EPI>(p, m0, n0, it0 + UNR, Bn);
     const size_t* o = B.o;
     const bool* ok = B.ok;
     const u32x4* ea = B.ea;
@@ -972,15 +999,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
       const float4* ps = (const float4*)(Pt + ci);
       const float4* ph = (const float4*)(Pt + p.C + ci);
       const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
-      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      const f32x2 sc[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
+      const f32x2 sh[4] = {{h0.x, h0.y}, {h0.z, h0.w}, {h1.x, h1.y}, {h1.z, h1.w}};
       u32x4 va[PCH];
 #pragma unroll
       for (int i = 0; i < PCH; ++i) va[i] = *(const u32x4*)(As + cur * BM * 64 + (tid + i * NT) * 8);
 #pragma unroll
       for (int i = 0; i < PCH; ++i)
         *(u32x4*)(As + cur * BM * 64 + (tid + i * NT) * 8) =
-            affine_relu8(va[i], sc, sh, true, p.pro_relu != 0);
+            affine_relu8_pk(va[i], sc, sh, p.pro_relu != 0);
       // raw barrier: __syncthreads() would also drain the next tile's DMA (vmcnt(0))
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1003,12 +1030,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
         const float4* ps = (const float4*)(Pt + ci);
         const float4* ph = (const float4*)(Pt + p.C + ci);
         const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
-        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        const f32x2 sc[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
+        const f32x2 sh[4] = {{h0.x, h0.y}, {h0.z, h0.w}, {h1.x, h1.y}, {h1.z, h1.w}};
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
           af[fm] = __builtin_bit_cast(
-              bf16x8, affine_relu8(__builtin_bit_cast(u32x4, af[fm]), sc, sh, true, p.pro_relu != 0));
+              bf16x8, affine_relu8_pk(__builtin_bit_cast(u32x4, af[fm]), sc, sh, p.pro_relu != 0));
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {

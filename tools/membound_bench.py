@@ -49,7 +49,7 @@ def main():
     mi = torch.cat([torch.randn(S, N, device=dev) * 0.1, torch.rand(S, N, device=dev) + 0.5]).reshape(-1)
     base = 2.0 * (M * K + M * N)
     for v in range(ops.igemm_nvariants()):
-        if a.only >= 0 and v != a.only:
+        if (a.only >= 0 and v != a.only) or not ops.igemm_variant_ok(v, g, False, False):
             continue
         bm = ops.igemm_variant_bm(v)
         glds = ops.igemm_variant_glds(v)
@@ -66,7 +66,7 @@ def main():
             x, w, y, None, st, g, None, None, 0, False, 4, r, None, v, None, mi, M // S, 0, 0, xa,
             mask, None, None, None, None, None)), base + 4.0 * M * N + M * N / 8)
         print(f"v{v:2d} {bm}x{ops.igemm_variant_bn(v)}{' glds' if glds else ''}: " +
-              "  ".join(f"{k} {t:6.1f}us {b / t / 1e3:5.2f}TB/s" for k, (t, b) in res.items()),
+              "  ".join(f"{k} {t:6.1f}us {b / t / 1e6:5.2f}TB/s" for k, (t, b) in res.items()),
               flush=True)
 
 
