@@ -2320,7 +2320,17 @@ int wgrad_splits(const ConvGeom& g, int variant) {
   // the patch kernel's K tile is all 9 taps of 64 input channels; its M unit is 256 rows
   const int tiles = ((g.N + bco - 1) / bco) * (patch ? g.C / 64 : (K + bkk - 1) / bkk);
   const int iters = patch ? M / 256 : (M + 63) / 64;
-  const int target = WG_VARIANTS[variant][2];
+  // The weight gradients run on their own stream beside the dgrad / BatchNorm chain, so they
+  // need not fill the chip alone, and every split costs an fp32 N x K slab written here and
+  // re-read by the split reduction: the step is fastest at ~60 % of the targets tuned for a
+  // weight gradient running alone (A/B of SIMCLR_WGRAD_TARGET_PCT, ResNet-50 step: 25 % 23.68,
+  // 35 % 22.98, 50 % 22.83, 70 % 22.74, 100 % 23.24, 200 % 23.16 ms)
+  static const int pct = [] {
+    const char* e = getenv("SIMCLR_WGRAD_TARGET_PCT");
+    const int v = e ? atoi(e) : 60;
+    return v > 0 ? v : 100;
+  }();
+  const int target = std::max(1, WG_VARIANTS[variant][2] * pct / 100);
   int splits = (target + tiles - 1) / tiles;
   int max_splits = patch ? iters : iters / 8;
   if (max_splits < 1) max_splits = 1;

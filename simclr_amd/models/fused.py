@@ -46,6 +46,11 @@ from ..ops.conv_hip import (fwd_geom, igemm_choose, igemm_launch, run_wgrad, sha
 from ..parallel import state as pstate
 
 
+# attribution experiment (never for training): SIMCLR_SKIP_WGRAD=1 drops the backbone's weight-
+# gradient kernels, exposing how much of the step the dgrad / BatchNorm chain alone takes
+_SKIP_WGRAD = os.environ.get("SIMCLR_SKIP_WGRAD", "0") == "1"
+
+
 def _empty_nhwc(n, h, w, c, dev, dtype=torch.bfloat16):
     return torch.empty((n, h, w, c), device=dev, dtype=dtype)
 
@@ -461,6 +466,9 @@ class FusedStages:
         dpro = (bnb[0], bnb[1], M // S, S) if bnb is not None else None
 
         def run():
+            if _SKIP_WGRAD:  # attribution experiment only: the step without weight gradients
+                _deliver_grad(cs.conv.weight, lambda out: None)
+                return
             _deliver_grad(cs.conv.weight,
                           lambda out: run_wgrad(ops, dyn, xn, out, g, C, pro=pro, dpro=dpro))
 
