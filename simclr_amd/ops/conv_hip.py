@@ -17,6 +17,7 @@ Pass decomposition (all on ``igemm_nt`` / ``wgrad_tn``):
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -141,6 +142,22 @@ def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=N
     return (stats, M // bm) if stats is not None else None
 
 
+def _parse_variants(spec):
+    """"a-b,c" -> {a..b, c}; None / empty -> None."""
+    if not spec:
+        return None
+    out = set()
+    for part in spec.split(","):
+        lo, _, hi = part.partition("-")
+        out.update(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+# SIMCLR_WGRAD_VARIANTS="lo-hi,...": autotune the weight gradients over these variants only
+# (attribution experiments: register-staged vs LDS-DMA tiles beside the dgrad chain)
+_WG_ONLY = _parse_variants(os.environ.get("SIMCLR_WGRAD_VARIANTS", ""))
+
+
 def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
     """Split-M weight gradient (fp32, written to ``out`` = OHWI) with the autotuned variant.
 
@@ -173,6 +190,8 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
     if v is None:
         cands = [v for v in range(ops.wgrad_nvariants())
                  if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)]
+        if _WG_ONLY is not None:  # experiment: restrict the candidates (fallback: all)
+            cands = [v for v in cands if v in _WG_ONLY] or cands
         v = tuning.pick(key, cands, 1 if N <= 64 else 0,
                         lambda vv: launch(vv, torch.empty_like(out)))
     launch(v, out)

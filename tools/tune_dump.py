@@ -21,3 +21,8 @@ ops = _ext.ops()
 for k, v in tuning.table().items():
     if k[0] == "igemm" and (k[7] or k[3] or "--all" in sys.argv):
         print("bnb" if k[7] else "pro" if k[3] else "dual" if k[8] else "-", "M=%d N=%d K=%d" % (k[1][0]*k[1][4]*k[1][5], k[1][14], k[1][6]*k[1][7]*k[1][3]), "epi", k[4], "->", v, "glds" if ops.igemm_variant_glds(v) else "nt", ops.igemm_variant_bm(v))
+    elif k[0] == "wgrad" and "--all" in sys.argv:
+        g = k[1]
+        print("wgrad", "M=%d N=%d K=%d" % (g[0] * g[4] * g[5], g[14], g[6] * g[7] * g[3]),
+              "pro" if k[3] else "-", "dpro" if k[4] else "-", "->", v,
+              "splits", ops.wgrad_splits(list(g), v))
