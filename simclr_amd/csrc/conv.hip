@@ -1857,15 +1857,33 @@ __global__ void wgrad_reduce(const float* __restrict__ partial, float* __restric
   }
 }
 
+// Sum of `cnt` float4 slabs `step` float4s apart (fixed order: four interleaved partial sums
+// combined at the end, so four independent loads are in flight per thread instead of one
+// dependent chain — the split reductions were latency-bound at ~20 us per call).
+__device__ __forceinline__ float4 slab_sum4(const float4* __restrict__ p, size_t step, int cnt) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, d = a;
+  int sp = 0;
+  for (; sp + 3 < cnt; sp += 4) {
+    const float4 v0 = p[(size_t)sp * step], v1 = p[(size_t)(sp + 1) * step];
+    const float4 v2 = p[(size_t)(sp + 2) * step], v3 = p[(size_t)(sp + 3) * step];
+    a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+    b.x += v1.x; b.y += v1.y; b.z += v1.z; b.w += v1.w;
+    c.x += v2.x; c.y += v2.y; c.z += v2.z; c.w += v2.w;
+    d.x += v3.x; d.y += v3.y; d.z += v3.z; d.w += v3.w;
+  }
+  for (; sp < cnt; ++sp) {
+    const float4 v = p[(size_t)sp * step];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  return make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
+                     (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
+}
+
 __global__ void wgrad_reduce_vec4(const float4* __restrict__ partial, float4* __restrict__ out,
                                   int splits, int sstride, size_t n4, float beta) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
-    float4 s = partial[i];
-    for (int sp = 1; sp < splits; ++sp) {
-      const float4 v = partial[(size_t)sp * sstride * n4 + i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
+    float4 s = slab_sum4(partial + i, (size_t)sstride * n4, splits);
     if (beta != 0.f) {
       const float4 o = out[i];
       s.x += beta * o.x; s.y += beta * o.y; s.z += beta * o.z; s.w += beta * o.w;
@@ -1873,23 +1891,13 @@ __global__ void wgrad_reduce_vec4(const float4* __restrict__ partial, float4* __
     out[i] = s;
   }
 }
-
-// Level 1 of a many-split reduction: slab g*group (+)= slabs g*group+1 .. g*group+group-1, in
-// place (each float4 index is owned by one thread), so the final pass reads splits/group slabs.
-// A small weight (few output tiles) gets hundreds of M-splits: summing them serially per output
-// element was latency-bound (tens of µs for a 16K-float gradient).
 __global__ void wgrad_reduce_l1(float4* __restrict__ partial, int splits, int group, size_t n4) {
   const int g = blockIdx.y;
   const int s0 = g * group;
   const int s1 = min(splits, s0 + group);
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
-    float4 s = partial[(size_t)s0 * n4 + i];
-    for (int sp = s0 + 1; sp < s1; ++sp) {
-      const float4 v = partial[(size_t)sp * n4 + i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    partial[(size_t)s0 * n4 + i] = s;
+    partial[(size_t)s0 * n4 + i] = slab_sum4(partial + (size_t)s0 * n4 + i, n4, s1 - s0);
   }
 }
 
