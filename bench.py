@@ -1,8 +1,12 @@
 """Headline benchmark: SimCLR pre-training images/sec (whole node), ResNet-50, CIFAR-10 shape.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
-``torch.distributed.run`` (one rank per GPU, RCCL).  W untimed steps, then exactly K timed steps
-bracketed by barrier + device synchronise, max over ranks, rank 0 prints ONE JSON line.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 either launched
+by ``torch.distributed.run`` (one rank per GPU, RCCL) or, when started directly (no
+``WORLD_SIZE`` in the environment), it spawns the N ranks itself through the fail-fast launcher
+(simclr_amd/runtime/launcher.py, the analogue of /root/reference/launch.py:202-259) before the
+parent touches the GPU.  Every rank asserts ``WORLD_SIZE == --gpus``.  W untimed steps, then
+exactly K timed steps bracketed by barrier + device synchronise, max over ranks, rank 0 prints
+ONE JSON line.
 
 Config (BASELINE.json "ResNet-50 SimCLR CIFAR-10 bf16, batch=512 on 1 MI355X"): ResNet-50 with
 the CIFAR stem (3x3/s1, no maxpool — the north star's CIFAR-ResNet-50), 512 images per GPU (two
@@ -18,6 +22,7 @@ BASELINE publishes no throughput, so that measurement is the ``vs_baseline`` den
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -31,6 +36,29 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "pretrain images/sec (whole node) + CIFAR-10 linear-probe top-1, ResNet-50"
+PG_TIMEOUT_S = float(os.environ.get("SIMCLR_BENCH_PG_TIMEOUT", "300"))
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args, argv) -> int:
+    """``--gpus N`` without a launcher: spawn N ranks of this script (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment) and return the first non-zero exit code (the
+    survivors are terminated) or 0.  Runs before any GPU call in this process; rank 0's JSON
+    line reaches stdout directly."""
+    from simclr_amd.runtime.launcher import launch, parse_args
+    ndev = torch.cuda.device_count()  # counts devices without initialising HIP in this process
+    if ndev and ndev < args.gpus and os.environ.get("SIMCLR_DIST_BACKEND") != "gloo":
+        raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} GPU(s) visible")
+    la = parse_args(["--nproc_per_node", str(args.gpus), "--master_addr", "127.0.0.1",
+                     "--master_port", str(_free_port()), "--use_env", str(Path(__file__).resolve()),
+                     *argv])
+    return launch(la)
 
 
 def _init():
@@ -53,7 +81,10 @@ def _init():
         # two ranks on the same device); the driver's runs use nccl (= RCCL over xGMI).
         be = os.environ.get("SIMCLR_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
         kw = {"device_id": dev} if be == "nccl" else {}
-        dist.init_process_group(be, rank=rank, world_size=world, **kw)
+        # short process-group timeout: a dead or hung rank fails the bench in minutes instead of
+        # holding the node for the default 30 min
+        dist.init_process_group(be, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=PG_TIMEOUT_S), **kw)
     return rank, world, local, dev
 
 
@@ -95,6 +126,8 @@ def run_ours(args, rank, world, dev):
     loader = ContrastiveLoader(ds, args.batch, dev, rank=rank, world=world,
                                strength=cfg["experiment"]["strength"], seed=7, views=2)
     tr = Trainer(cfg, st, 50000)
+    args.dtype = tr.precision  # fp32 on a CPU rehearsal
+    tr.guard.on_error = "defer"  # an IPC timeout is checked collectively below (ipc_guard)
     it = iter(loader)
     args.bn_comm = ("ipc" if st.ipc is not None else "rccl") if st.comm else "none"
 
@@ -156,7 +189,8 @@ def run_ours(args, rank, world, dev):
         # experiment: the step's main stream at the highest priority (side streams stay low)
         lo, hi = torch.cuda.Stream.priority_range()
         ctx = torch.cuda.stream(torch.cuda.Stream(device=dev, priority=hi))
-    with ctx:
+    def measure():
+        nonlocal loss
         for _ in range(args.warmup):
             loss = tr.step(next_batch())
         _sync(dev, world)
@@ -174,12 +208,22 @@ def run_ours(args, rank, world, dev):
             host += time.perf_counter() - h0
         _sync(dev, world)
         t1 = time.perf_counter()
-    # host time spent issuing the steps (≈ wall time means the run is launch/CPU bound)
-    args.host_issue_ms = host / args.steps * 1000.0
-    if st.ipc is not None and st.ipc.failed():  # a spin timed out: statistics were wrong
-        print(f"[bench] rank {rank}: IPC statistics exchange timed out", file=sys.stderr,
-              flush=True)
-        args.bn_comm = "ipc-timeout"
+        # host time spent issuing the steps (≈ wall time means the run is launch/CPU bound)
+        args.host_issue_ms = host / args.steps * 1000.0
+        return t0, t1
+
+    with ctx:
+        t0, t1 = measure()
+        if ipc_guard():
+            # an IPC spin timed out inside the timed region: those steps ran on partial
+            # BatchNorm statistics, so the measurement is void — every rank is on RCCL now
+            # (collective decision) and the K steps are timed again
+            print(f"[bench] rank {rank}: IPC statistics exchange timed out in the timed region; "
+                  "re-timing on RCCL", file=sys.stderr, flush=True)
+            tr.graph = None
+            args.graph = False
+            args.bn_comm = "rccl(ipc-timeout, re-timed)"
+            t0, t1 = measure()
 
     return t1 - t0, float(loss.item()) if loss is not None else float("nan")
 
@@ -257,8 +301,14 @@ def main(argv=None):
                     help="issue every step eagerly (default: probe both, keep the faster)")
     ap.add_argument("--bucket-mb", dest="bucket_mb", type=float, default=32.0)
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = ap.parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, argv))
     rank, world, local, dev = _init()
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and "
+                         "the flag disagree")
     if args.gather is None:
         args.gather = world > 1
     if args.graph is None:
@@ -302,7 +352,7 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": (round(value / base, 3) if (base and args.impl == "ours") else None),
-        "dtype": args.precision if args.impl == "ours" else "fp32",
+        "dtype": getattr(args, "dtype", args.precision) if args.impl == "ours" else "fp32",
         "data": (f"synthetic {args.size}x{args.size} uint8 "
                  f"{'CIFAR' if args.size == 32 else 'ImageNet'}-shape images, random-init "
                  "weights, on-device SimCLR augmentation"),

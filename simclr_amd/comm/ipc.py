@@ -12,8 +12,10 @@ own arena in rank order (csrc/bn.hip ``bn_ipc_exchange``) — one kernel per Bat
 RCCL, no host involvement, capturable in the step's hipGraph, bitwise-identical statistics on
 every rank.
 
-Arena layout: int64 words; every BatchNorm site (a (module, direction) pair, allocated in
-first-call order, which is identical on all ranks of an SPMD step) owns
+Arena layout: int64 words; every BatchNorm site (a (module name, direction, shape) key —
+``site_key``: the module's qualified name inside its model, so a model rebuilt in the same
+process reuses its sites instead of leaking arena space — allocated in first-call order, which
+is identical on all ranks of an SPMD step) owns
 ``2 parities x world x [2][S][C]`` words at the same offset in every rank's arena, and
 ``ceil(C/64)`` epoch counters in a local int32 buffer.
 
@@ -31,6 +33,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _ext
+from ..parallel.state import site_key, tag_sites  # noqa: F401
 
 DEFAULT_WORDS = 1 << 23  # 64 MiB arena: ResNet-50 fwd + bwd sites at W = 8 need ~30 MiB
 MAX_WORLD = 16
@@ -53,12 +56,12 @@ class SiteTable:
         self.next_epoch = 0
 
     def get(self, key, S: int, C: int) -> Tuple[int, int, int]:
-        """(word offset, epoch offset, epoch count) of ``key``'s region (allocated on first use;
-        a key seen again with another shape is an error: the peers hold the old layout)."""
+        """(word offset, epoch offset, epoch count) of ``key``'s region at shape (S, C),
+        allocated on first use (the same name at another shape — e.g. ResNet-18 then ResNet-50
+        in one process — gets a region of its own)."""
+        key = (key, S, C)
         if key in self.sites:
-            off, eo, ne, shape = self.sites[key]
-            if shape != S * 100000 + C:
-                raise ValueError(f"IPC site {key!r} reused with another shape (S={S}, C={C})")
+            off, eo, ne, _ = self.sites[key]
             return off, eo, ne
         n = region_words(self.world, S, C)
         ne = (C + 63) // 64
@@ -211,3 +214,57 @@ def fallback_if_failed(st, device: torch.device) -> bool:
           file=sys.stderr, flush=True)
     st.ipc = None
     return True
+
+
+class IpcExchangeError(RuntimeError):
+    """An IPC BatchNorm-statistics exchange timed out: that step ran on partial statistics."""
+
+
+# eager steps that run with the BatchNorm statistics on RCCL (not the IPC exchange): every rank
+# autotunes its conv tiles during its first step(s), seconds apart, which would exceed the IPC
+# exchange's 2 s spin bound; afterwards the ranks adopt rank 0's tuning table
+TUNING_STEPS = 2
+
+
+class StepGuard:
+    """Wraps the eager training step of a loop that may use the IPC exchange.
+
+    * the first ``TUNING_STEPS`` steps run with ``st.ipc`` detached (statistics over RCCL) and
+      end with ``tuning.sync_from_rank0`` — identical tiles on every rank;
+    * after every step the exchange's sticky error flag is copied into pinned host memory
+      (async, no sync) and the copy of the previous step is read: ``on_error="raise"`` raises
+      ``IpcExchangeError`` (the fail-fast launcher then stops every rank — training never runs on
+      from partial statistics), ``"defer"`` leaves the check to the caller (bench.py)."""
+
+    def __init__(self, st, on_error: str = "raise"):
+        self.st = st
+        self.on_error = on_error
+        self.eager_steps = 0
+        self._err_host: Optional[torch.Tensor] = None
+
+    def run(self, body, *a):
+        if self.eager_steps >= TUNING_STEPS or not self.st.comm:
+            self.eager_steps += 1
+            return body(*a)
+        ipc, self.st.ipc = self.st.ipc, None
+        try:
+            out = body(*a)
+        finally:
+            self.st.ipc = ipc
+        self.eager_steps += 1
+        from ..ops import tuning
+        tuning.sync_from_rank0(self.st.group)
+        return out
+
+    def check(self, step: int = -1) -> None:
+        ipc = self.st.ipc
+        if ipc is None:
+            return
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32,
+                                         pin_memory=ipc.err.is_cuda)
+        elif self.on_error == "raise" and int(self._err_host[0]) != 0:
+            raise IpcExchangeError(
+                f"rank {self.st.rank}: IPC BatchNorm-statistics exchange timed out at or before "
+                f"step {step}; stopping (that step's statistics were partial)")
+        self._err_host.copy_(ipc.err, non_blocking=True)

@@ -103,7 +103,9 @@ __global__ void k_maxpool_bwd(const uint16_t* __restrict__ dy, const uint8_t* __
 
 // ---------------------------------------------------------------------------- CE + top-k
 // logits [B][C] fp32, y [B] int64.  Per row: loss = lse - logit[y]; rank = #{j: logit[j] >
-// logit[y]} + #{j < y: logit[j] == logit[y]}; dlogits (optional) = (softmax - onehot)·gscale.
+// logit[y]} + #{j < y: logit[j] == logit[y]} + #{j != y: logit[j] is NaN} (torch.topk orders NaN
+// above every number); a NaN target logit or an out-of-range label gives rank C (never correct);
+// dlogits (optional) = (softmax - onehot)·gscale.
 // One 64-lane wave per row, 4 rows per block.
 __global__ __launch_bounds__(256) void k_ce_topk(const float* __restrict__ logits,
                                                  const int64_t* __restrict__ y, int B, int C,
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256) void k_ce_topk(const float* __restrict__ logit
   int above = 0;
   for (int j = lane; j < C; j += 64) {
     const float v = z[j];
-    above += (v > zt || (v == zt && j < t)) ? 1 : 0;
+    above += (v > zt || (v == zt && j < t) || (v != v && j != t)) ? 1 : 0;
     if (v > m) { s = s * __expf(m - v) + 1.f; m = v; } else { s += __expf(v - m); }
   }
   // wave reduction of (m, s) and the count
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(256) void k_ce_topk(const float* __restrict__ logit
   }
   const float lse = m + __logf(s);
   if (lane == 0) {
-    const bool valid = t >= 0 && t < C;
+    const bool valid = t >= 0 && t < C && zt == zt;
     loss[row] = lse - zt;             // NaN for an out-of-range label (as F.cross_entropy errors)
     rank[row] = valid ? above : C;    // never counted as correct
   }

@@ -14,6 +14,7 @@ from typing import Optional
 import torch
 from torch import nn
 
+from ..parallel.state import tag_sites
 from .heads import ProjectionHead
 from .resnet import build_backbone
 
@@ -27,6 +28,7 @@ class ContrastiveModel(nn.Module):
                                 cifar_stem=cifar_stem, stem_padding=stem_padding)
         num_last_hidden_units = self.f.num_features
         self.g = ProjectionHead(num_last_hidden_units, d)
+        tag_sites(self)  # stable IPC exchange-site names (comm/ipc.py)
 
     def encode(self, inputs: torch.Tensor, segments: int = 1) -> torch.Tensor:
         return self.f(inputs, segments=segments)  # N x H
@@ -43,6 +45,7 @@ class SupervisedModel(nn.Module):
         assert base_cnn in {"resnet18", "resnet50"}
         self.f = build_backbone(base_cnn, num_classes=num_classes, is_cifar=is_cifar,
                                 cifar_stem=cifar_stem, stem_padding=stem_padding)
+        tag_sites(self)
 
     def forward(self, inputs: torch.Tensor, segments: int = 1) -> torch.Tensor:
         return self.f(inputs, segments=segments)

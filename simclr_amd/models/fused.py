@@ -44,6 +44,7 @@ import torch.distributed as dist
 from ..ops import _ext
 from ..ops.conv_hip import (fwd_geom, igemm_choose, igemm_launch, run_wgrad, shadow_ohwi)
 from ..parallel import state as pstate
+from ..parallel.state import site_key
 
 
 # attribution experiment (never for training): SIMCLR_SKIP_WGRAD=1 drops the backbone's weight-
@@ -254,7 +255,7 @@ class FusedStages:
              bn.weight.detach(), bn.bias.detach() if mode == 1 else None, dgamma, dbeta, coef]
         ints = [0, 1, 0, slot]
         if st.ipc is not None:
-            kw = st.ipc.kwargs((id(bn), "fwd" if mode == 1 else "bwd"), S, C)
+            kw = st.ipc.kwargs(site_key(bn, "fwd" if mode == 1 else "bwd"), S, C)
             t += [kw["ipc_peers"], kw["ipc_arena"], kw["ipc_epoch"], kw["ipc_err"]]
             ints = [kw["ipc_site"], kw["world"], kw["rank"], slot]
         return (mode, t, [count, bn.eps if mode == 1 else 0.0,
@@ -353,7 +354,7 @@ class FusedStages:
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
                                 bn.weight.detach(), bn.bias.detach(), ss, None, None, None, slot,
-                                **(ipc.kwargs((id(bn), "fwd"), S, C) if ipc is not None else {}),
+                                **(ipc.kwargs(site_key(bn, "fwd"), S, C) if ipc is not None else {}),
                                 zero_after=zero)
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
@@ -435,7 +436,7 @@ class FusedStages:
             # single launch; with the IPC exchange dγ, dβ come from the local sums and coef
             # from the global ones (SyncBN semantics, see _bn_bwd_start)
             partial, nblk_seg, ipc = h[2], h[3], h[5]
-            kw = ipc.kwargs((id(bn), "bwd"), S, C) if ipc is not None else {}
+            kw = ipc.kwargs(site_key(bn, "bwd"), S, C) if ipc is not None else {}
             self._deliver_bn_grads(bn, lambda dg, db: ops.bn_reduce_fused(
                 partial, abs(nblk_seg), S, C, 2, None, bs.count, 0.0, 0.0, None, None, bs.mi,
                 None, bn.weight.detach(), None, None, dg, db, coef, **kw,

@@ -14,6 +14,7 @@ import torch
 import torch.distributed as dist
 
 from . import _ext
+from ..parallel.state import site_key
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -67,7 +68,7 @@ class BatchNormHipFn(torch.autograd.Function):
         if not st.comm or ipc is not None:  # one launch (the IPC exchange runs inside it)
             ops.bn_reduce_fused(partial, nblk, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
-                                **(ipc.kwargs((id(bn), "fwd"), S, C) if ipc is not None else {}))
+                                **(ipc.kwargs(site_key(bn, "fwd"), S, C) if ipc is not None else {}))
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
             ops.bn_reduce_fused(partial, nblk, S, C, 0, stats)
@@ -80,7 +81,7 @@ class BatchNormHipFn(torch.autograd.Function):
         ctx.save_for_backward(x, y if relu else None, mi, weight)
         ctx.cfg = (S, relu, residual is not None, count, st)
         ctx.bias = bias
-        ctx.bn_key = id(bn)  # the BatchNorm's IPC exchange site (stable across steps)
+        ctx.bn_key = site_key(bn, "bwd")  # the BatchNorm's IPC exchange site
         return y
 
     @staticmethod
@@ -108,7 +109,7 @@ class BatchNormHipFn(torch.autograd.Function):
             # coefficients from the global ones
             ops.bn_reduce_fused(partial, nblk, S, C, 2, None, count, 0.0, 0.0, None, None, mi,
                                 None, weight.detach(), None, None, dgamma, dbeta, coef,
-                                **(ipc.kwargs((ctx.bn_key, "bwd"), S, C) if ipc is not None
+                                **(ipc.kwargs(ctx.bn_key, S, C) if ipc is not None
                                    else {}))
         else:
             # dγ, dβ from the LOCAL sums (the data-parallel reducer sums them across ranks,

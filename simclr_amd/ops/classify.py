@@ -22,7 +22,10 @@ def _hip_ok(logits: torch.Tensor) -> bool:
 
 
 def ce_rank(logits: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(per-row CE loss fp32, per-row rank of the target) — rank 0 means top-1 correct."""
+    """(per-row CE loss fp32, per-row rank of the target) — rank 0 means top-1 correct.
+
+    Ties go to the lower class index; a NaN logit of another class ranks above the target (the
+    order ``torch.topk`` uses) and a NaN target logit gets rank C, i.e. it is never correct."""
     logits = logits.float().contiguous()
     y = y.to(device=logits.device, dtype=torch.long).contiguous()
     if _hip_ok(logits):
@@ -34,8 +37,11 @@ def ce_rank(logits: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.
     loss = F.cross_entropy(logits, y, reduction="none")
     zt = logits.gather(1, y.view(-1, 1))
     idx = torch.arange(logits.shape[1], device=logits.device).view(1, -1)
-    above = (logits > zt) | ((logits == zt) & (idx < y.view(-1, 1)))
-    return loss, above.sum(1).to(torch.int32)
+    above = (logits > zt) | ((logits == zt) & (idx < y.view(-1, 1))) | \
+        (torch.isnan(logits) & (idx != y.view(-1, 1)))  # torch.topk: NaN ranks above numbers
+    rank = above.sum(1).to(torch.int32)
+    # a NaN target logit (diverged probe, empty-class centroid) is never counted as correct
+    return loss, torch.where(torch.isnan(zt.view(-1)), logits.shape[1], rank).to(torch.int32)
 
 
 class _CEHipFn(torch.autograd.Function):

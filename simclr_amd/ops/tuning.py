@@ -69,3 +69,22 @@ def pick(key: Hashable, candidates: Sequence[int], default: int,
 
 def table() -> Dict[Hashable, int]:
     return dict(_CACHE)
+
+
+def sync_from_rank0(group=None) -> int:
+    """Adopt rank 0's choices on every rank (collective; call it on all ranks after the eager
+    steps that tuned).  Each rank times its candidates on its own GPU, so near-ties can resolve
+    differently and the ranks would run different tiles — different fp32 summation orders —
+    where the reference pins one algorithm everywhere (``cudnn.deterministic=True,
+    benchmark=False``, /root/reference/main.py:150-151).  Returns the number of entries this
+    rank changed."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) < 2:
+        return 0
+    obj = [dict(_CACHE) if dist.get_rank(group) == 0 else None]
+    dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None
+                               else 0, group=group)
+    theirs = obj[0] or {}
+    changed = sum(1 for k, v in theirs.items() if _CACHE.get(k) != v)
+    _CACHE.update(theirs)
+    return changed

@@ -10,6 +10,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+import torch
 import torch.distributed as dist
 
 
@@ -82,3 +83,19 @@ def rank() -> int:
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(_STATE.group)
     return 0
+
+
+def tag_sites(model: torch.nn.Module) -> None:
+    """Name every BatchNorm of ``model`` after its qualified module name (the IPC site key)."""
+    for name, m in model.named_modules():
+        if hasattr(m, "running_mean") and hasattr(m, "num_features"):  # ours and torch's BN
+            m._site_name = name
+
+
+def site_key(bn: torch.nn.Module, direction: str):
+    """Stable exchange-site key of a BatchNorm (``tag_sites``; an untagged module falls back
+    to its object identity)."""
+    name = bn.__dict__.get("_site_name")
+    if name is None:
+        name = f"untagged-{type(bn).__name__}-{id(bn)}"
+    return (name, direction)

@@ -27,6 +27,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from ..comm.ipc import StepGuard
 from ..config import check_pretrain_conf
 from ..data.datasets import load_dataset
 from ..data.loader import ContrastiveLoader
@@ -38,7 +39,7 @@ from ..optim.schedule import MODE_WARMUP_COSINE, calculate_initial_lr
 from ..parallel.flat import FlatParamStore
 from ..runtime.dist import init_distributed
 from ..utils.checkpoint import checkpoint_name, save_reference_checkpoint, save_resume, load_resume
-from ..utils.misc import cfg_get, seed_everything, MetricsWriter
+from ..utils.misc import cfg_get, seed_everything, MetricsWriter, refuse_experiment_knobs
 
 log = logging.getLogger(__name__)
 
@@ -57,7 +58,11 @@ def build_contrastive_model(cfg, device, precision: str):
 
 
 class Trainer:
-    """Owns model, flat store, optimizer, loss and the (optionally graph-captured) step."""
+    """Owns model, flat store, optimizer, loss and the (optionally graph-captured) step.
+
+    ``guard`` (comm/ipc.py ``StepGuard``): RCCL statistics + rank-0 tuning table for the first
+    eager steps, and the per-step check of the IPC exchange's error flag (``guard.on_error``:
+    ``"raise"`` in training, ``"defer"`` in bench.py, which checks collectively)."""
 
     def __init__(self, cfg, st, dataset_len: int, precision: Optional[str] = None):
         self.cfg = cfg
@@ -86,6 +91,7 @@ class Trainer:
         self.graph = None
         self._static_x = None
         self._static_loss = None
+        self.guard = StepGuard(st)
 
     def prepare(self, x: torch.Tensor) -> torch.Tensor:
         if self.precision == "bf16" and self.device.type == "cuda":
@@ -105,14 +111,20 @@ class Trainer:
         self.opt.step()
         return loss.detach()
 
+    def _eager(self, x: torch.Tensor) -> torch.Tensor:
+        return self.guard.run(self._step_body, x)
+
     def step(self, x: torch.Tensor) -> torch.Tensor:
         x = self.prepare(x)
         if self.graph is not None:
             self._static_x.copy_(x)
             self.graph.replay()
             self.opt.host_step += 1
-            return self._static_loss
-        return self._step_body(x)
+            loss = self._static_loss
+        else:
+            loss = self._eager(x)
+        self.guard.check(self.opt.host_step)
+        return loss
 
     def capture(self, x: torch.Tensor, warmup: int = 2) -> None:
         """Capture one full training step into a hipGraph (after ``warmup`` eager steps)."""
@@ -121,7 +133,7 @@ class Trainer:
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self._step_body(x)
+                self._eager(x)
         torch.cuda.current_stream(self.device).wait_stream(s)
         if self.st.comm:
             # the RCCL watchdog polls the end events of the eager warm-up collectives; HIP refuses
@@ -142,6 +154,7 @@ class Trainer:
 
 
 def pretrain(cfg) -> dict:
+    refuse_experiment_knobs("pretrain")
     st = init_distributed(cfg, use_cuda=cfg["parameter"].get("use_cuda", True))
     check_pretrain_conf(cfg)
     registry.set_backend(cfg_get(cfg, "runtime.backend", "auto"))
@@ -216,12 +229,7 @@ def pretrain(cfg) -> dict:
         if st.device.type == "cuda":
             torch.cuda.synchronize()
         dt = max(time.time() - t0, 1e-9)
-        if st.ipc is not None:
-            from simclr_amd.comm import fallback_if_failed
-            if fallback_if_failed(st, st.device):
-                log.error("epoch %d: IPC BatchNorm-statistics exchange timed out (statistics of "
-                          "that step were partial); switched to RCCL", epoch)
-                tr.graph = None
+        tr.guard.check(step_global)  # the epoch's last step (its flag copy has landed)
         imgs = nsteps * cfg["experiment"]["batches"] * st.world_size
         summary.update(epochs_run=summary["epochs_run"] + 1, steps=step_global)
         if rank == 0:

@@ -19,19 +19,20 @@ import time
 
 import torch
 import torch.distributed as dist
-import torch.nn.functional as F
 
+from ..comm.ipc import StepGuard
 from ..config import check_supervised_conf
 from ..data.datasets import load_dataset
 from ..data.loader import ContrastiveLoader
 from ..models.contrastive import SupervisedModel
 from ..ops import registry
+from ..ops.classify import ce_rank, cross_entropy
 from ..optim.lars import FusedLARS
 from ..optim.schedule import MODE_WARMUP_COSINE, calculate_initial_lr
 from ..parallel.flat import FlatParamStore
 from ..runtime.dist import init_distributed
 from ..utils.checkpoint import checkpoint_name, save_reference_checkpoint
-from ..utils.misc import MetricsWriter, cfg_get, seed_everything
+from ..utils.misc import MetricsWriter, cfg_get, refuse_experiment_knobs, seed_everything
 
 log = logging.getLogger(__name__)
 
@@ -50,13 +51,17 @@ def validation(model, loader, precision, device):
     correct = torch.zeros(1, device=device, dtype=torch.float64)
     for x, y in loader:
         out = model(_prep(x, precision, device)).float()
-        sum_loss += F.cross_entropy(out, y, reduction="sum").double()
-        correct += (out.argmax(dim=1) == y).sum().double()
+        # one HIP kernel (csrc/eval.hip ce_topk) gives per-row CE and the target's rank;
+        # rank 0 <=> argmax == y (ties to the lower class, as argmax)
+        loss, rank = ce_rank(out, y)
+        sum_loss += loss.sum().double()
+        correct += (rank == 0).sum().double()
     model.train()
     return sum_loss, correct
 
 
 def supervised(cfg) -> dict:
+    refuse_experiment_knobs("supervised")
     check_supervised_conf(cfg)
     st = init_distributed(cfg, use_cuda=cfg["parameter"].get("use_cuda", True))
     registry.set_backend(cfg_get(cfg, "runtime.backend", "auto"))
@@ -105,18 +110,25 @@ def supervised(cfg) -> dict:
     loss = torch.zeros(())
     summary = {}
     model.train()
+    guard = StepGuard(st)  # RCCL statistics while tuning, per-step IPC error check
+
+    def train_step(x, y):
+        out = model(_prep(x, precision, dev)).float()
+        loss = cross_entropy(out, y)  # HIP CE kernel: the forward also writes the gradient
+        if not hip:
+            store.zero_grad()
+        loss.backward()
+        store.finish()
+        opt.step()
+        return loss
+
     for epoch in range(1, epochs + 1):
         train_loader.set_epoch(epoch)
         t0 = time.time()
         for x, y in train_loader:
-            out = model(_prep(x, precision, dev)).float()
-            loss = F.cross_entropy(out, y)
-            if not hip:
-                store.zero_grad()
-            loss.backward()
-            store.finish()
-            opt.step()
+            loss = guard.run(train_step, x, y)
             step += 1
+            guard.check(step)
             if max_steps is not None and step >= max_steps:
                 break
         line = None

@@ -79,8 +79,32 @@ def save_resume(path: str, model: nn.Module, optimizer, epoch: int, step: int,
         "epoch": int(epoch),
         "step": int(step),
         "torch_rng": torch.get_rng_state(),
+        "cuda_rng": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else [],
+        "numpy_rng": _numpy_rng_state(),
         "extra": extra or {},
     }, path)
+
+
+def _numpy_rng_state() -> dict:
+    """NumPy's global MT19937 state as tensors / ints (loadable with ``weights_only=True``)."""
+    import numpy as np
+    name, keys, pos, has_gauss, gauss = np.random.get_state()
+    return {"keys": torch.from_numpy(keys.astype(np.int64)), "pos": int(pos),
+            "has_gauss": int(has_gauss), "gauss": float(gauss)}
+
+
+def restore_rng(blob: dict) -> None:
+    """Restore the host / device / NumPy generators saved by ``save_resume``."""
+    import numpy as np
+    if blob.get("torch_rng") is not None:
+        torch.set_rng_state(blob["torch_rng"])
+    cuda = blob.get("cuda_rng") or []
+    if cuda and torch.cuda.is_available() and len(cuda) == torch.cuda.device_count():
+        torch.cuda.set_rng_state_all(cuda)
+    n = blob.get("numpy_rng")
+    if n:
+        np.random.set_state(("MT19937", n["keys"].numpy().astype(np.uint32), n["pos"],
+                             n["has_gauss"], n["gauss"]))
 
 
 def load_resume(path, model: nn.Module, optimizer=None, store=None) -> dict:
@@ -94,4 +118,5 @@ def load_resume(path, model: nn.Module, optimizer=None, store=None) -> dict:
         store.refresh_shadow()
     if optimizer is not None and blob.get("optimizer") is not None:
         optimizer.load_state_dict(blob["optimizer"])
+    restore_rng(blob)
     return blob

@@ -51,3 +51,17 @@ class MetricsWriter:
         if self.f is not None:
             self.f.close()
             self.f = None
+
+
+# attribution knobs that change the math (bench / tools only): a leftover export in a training
+# shell would silently train a wrong model
+EXPERIMENT_KNOBS = ("SIMCLR_SKIP_WGRAD", "SIMCLR_EXPERIMENT_SKIP_BNRED")
+
+
+def refuse_experiment_knobs(where: str) -> None:
+    import os
+    bad = [k for k in EXPERIMENT_KNOBS if os.environ.get(k, "0") not in ("", "0")]
+    if bad:
+        raise RuntimeError(f"{where}: {', '.join(bad)} set — these attribution experiments drop "
+                           "weight gradients / BatchNorm statistics and are refused outside "
+                           "bench.py and tools/")

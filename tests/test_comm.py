@@ -15,8 +15,71 @@ def test_site_table_is_first_call_order_and_stable():
     assert offs_a[0] == (0, 0, 1)
     assert offs_a[1] == (region_words(8, 2, 64), 1, 4)
     assert a.get(("bn1", "fwd"), 2, 64) == offs_a[0]  # stable on reuse
-    with pytest.raises(ValueError):
-        a.get(("bn1", "fwd"), 2, 128)  # peers hold the old layout
+    # the same module name at another shape (another model built in this process) gets a new
+    # region; the old one stays where the peers expect it
+    other = a.get(("bn1", "fwd"), 2, 128)
+    assert other[0] >= offs_a[2][0] + region_words(8, 2, 256)
+    assert a.get(("bn1", "fwd"), 2, 64) == offs_a[0]
+
+
+def test_site_keys_are_module_names_and_survive_rebuild():
+    """IPC sites are keyed by qualified module name (not id()): a model rebuilt in the same
+    process maps onto the same arena regions instead of leaking new ones."""
+    from simclr_amd.models.contrastive import ContrastiveModel, SupervisedModel
+    from simclr_amd.parallel.state import site_key
+    t = SiteTable(2, 1 << 22, 1 << 12)
+
+    def alloc(m):
+        return [t.get(site_key(bn, d), 2, bn.num_features)
+                for bn in m.modules() if hasattr(bn, "running_mean") for d in ("fwd", "bwd")]
+    m1 = ContrastiveModel("resnet18")
+    a1 = alloc(m1)
+    used = t.next_word
+    a2 = alloc(ContrastiveModel("resnet18"))
+    assert a1 == a2 and t.next_word == used
+    assert site_key(m1.f.layer2[0].downsample[1], "fwd") == ("f.layer2.0.downsample.1", "fwd")
+    assert site_key(SupervisedModel("resnet18").f.bn1, "bwd") == ("f.bn1", "bwd")
+
+
+class _FakeIpc:
+    def __init__(self):
+        import torch
+        self.err = torch.zeros(1, dtype=torch.int32)
+
+
+class _FakeSt:
+    comm, rank, group = True, 0, None
+
+    def __init__(self):
+        self.ipc = _FakeIpc()
+
+
+def test_step_guard_tuning_steps_detach_ipc(monkeypatch):
+    from simclr_amd.comm import ipc as ipcmod
+    from simclr_amd.ops import tuning
+    monkeypatch.setattr(tuning, "sync_from_rank0", lambda group=None: 0)
+    st = _FakeSt()
+    g = ipcmod.StepGuard(st)
+    seen = [g.run(lambda: st.ipc is None) for _ in range(ipcmod.TUNING_STEPS + 2)]
+    assert seen == [True] * ipcmod.TUNING_STEPS + [False, False]
+    assert st.ipc is not None
+
+
+def test_step_guard_raises_on_exchange_timeout():
+    """A timed-out exchange (sticky device flag) stops training at the next step instead of
+    running on partial BatchNorm statistics until the epoch ends."""
+    from simclr_amd.comm.ipc import IpcExchangeError, StepGuard
+    st = _FakeSt()
+    g = StepGuard(st)
+    g.check(0)
+    g.check(1)  # flag clear
+    st.ipc.err.fill_(1)
+    g.check(2)  # copies the set flag (asynchronously on a GPU)
+    with pytest.raises(IpcExchangeError):
+        g.check(3)
+    d = StepGuard(st, on_error="defer")
+    d.check(0)
+    d.check(1)  # deferred: the caller (bench.py) checks collectively
 
 
 def test_site_table_exhaustion():
@@ -72,3 +135,36 @@ def test_timeout_fallback_is_collective(tmp_path):
     mp.spawn(_fallback_worker, args=(3, port, str(tmp_path)), nprocs=3, join=True)
     for r in range(3):
         assert (tmp_path / f"fb{r}").read_text() == "1 1 0"
+
+
+def _tuning_worker(rank, world, port, out_dir):
+    import os
+    import torch.distributed as dist
+    from simclr_amd.ops import tuning
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tuning._CACHE.clear()
+    # each rank timed the same shapes on its own GPU: near-ties resolved differently
+    tuning._CACHE.update({("igemm", (1, 2, 3)): rank, ("wgrad", (4, 5)): 7,
+                          ("igemm", (9,)): 3 + rank})
+    changed = tuning.sync_from_rank0()
+    with open(os.path.join(out_dir, f"t{rank}"), "w") as f:
+        f.write(repr((sorted(tuning.table().items()), changed)))
+    dist.destroy_process_group()
+
+
+def test_tuning_tables_identical_across_ranks(tmp_path):
+    """After the tuning steps every rank runs rank 0's tile choices (the reference pins one
+    algorithm everywhere: cudnn.deterministic, /root/reference/main.py:150-151)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_tuning_worker, args=(3, port, str(tmp_path)), nprocs=3, join=True)
+    got = [eval((tmp_path / f"t{r}").read_text()) for r in range(3)]
+    assert got[0][0] == got[1][0] == got[2][0]
+    assert dict(got[0][0])[("igemm", (1, 2, 3))] == 0
+    assert [g[1] for g in got] == [0, 2, 2]

@@ -98,3 +98,26 @@ def test_imagenet_stem_resnet50_uses_hip_maxpool():
         assert bool(torch.isfinite(store.grad).all())
     finally:
         pooling_hip.MaxPoolHipFn.forward = staticmethod(orig)
+
+
+def _topk_correct(z, y, k):
+    return (torch.topk(z, k, dim=1)[1] == y[:, None]).any(1)
+
+
+def test_ce_topk_nan_logits_follow_torch_topk():
+    """A diverged probe (NaN logits) must not read as 100 % accurate: a NaN target logit is
+    never correct and a NaN of another class ranks above the target (torch.topk's order)."""
+    from simclr_amd.ops.classify import ce_rank
+    _ops()
+    torch.manual_seed(3)
+    B, C = 256, 10
+    z = torch.randn(B, C, device=DEV)
+    y = torch.randint(0, C, (B,), device=DEV)
+    z[:64] = float("nan")                                  # whole rows NaN
+    z[64:128, 3] = float("nan")                            # one NaN class per row
+    z[128:160].scatter_(1, y[128:160, None], float("nan"))  # NaN target logit only
+    _, rank = ce_rank(z, y)
+    nan_t = torch.isnan(z.gather(1, y[:, None])).view(-1)
+    assert bool((rank[nan_t] == C).all())  # topk may pick a NaN target: we never count it
+    for k in (1, 5):
+        assert torch.equal((rank < k)[~nan_t], _topk_correct(z, y, k)[~nan_t]), k

@@ -87,3 +87,20 @@ def test_cifar_binary_reader(tmp_path):
     assert len(te) == 4
     with pytest.raises(FileNotFoundError):
         load_dataset("cifar100", root=str(tmp_path))
+
+
+def test_ce_rank_fallback_nan_matches_topk():
+    from simclr_amd.ops.classify import ce_rank
+    torch.manual_seed(3)
+    B, C = 128, 10
+    z = torch.randn(B, C)
+    y = torch.randint(0, C, (B,))
+    z[:32] = float("nan")
+    z[32:64, 3] = float("nan")
+    z[64:80].scatter_(1, y[64:80, None], float("nan"))
+    _, rank = ce_rank(z, y)
+    nan_t = torch.isnan(z.gather(1, y[:, None])).view(-1)
+    assert bool((rank[nan_t] == C).all())  # topk may pick a NaN target: we never count it
+    for k in (1, 5):
+        ref = (torch.topk(z, k, dim=1)[1] == y[:, None]).any(1)
+        assert torch.equal((rank < k)[~nan_t], ref[~nan_t]), k
