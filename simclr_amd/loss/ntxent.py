@@ -6,9 +6,11 @@ views; for each, the logits are cosine similarities / τ to every other row (sel
 target is the same image's other view; ``reduction="mean"`` averages over the 2N anchors,
 ``"sum"`` sums, ``"none"`` returns a (2, N) tensor [view0 anchors; view1 anchors].
 
-Extension (north star): ``gather=True`` all-gathers ẑ from every rank over RCCL, so
-each anchor sees 2·N·W − 1 candidates instead of 2N − 1 (negatives from the global batch).  The
-gradient w.r.t. other ranks' columns flows back through an all-reduce of the column gradients.
+Extension (north star): ``gather=True`` all-gathers the bf16 embeddings z of every
+rank over RCCL (each rank then normalises all of them), so each anchor sees 2·N·W − 1
+candidates instead of 2N − 1 (negatives from the global batch).  The gradient w.r.t. the
+gathered columns returns through a reduce-scatter on a side stream, overlapped with the
+row-gradient kernel.
 Parity default is ``gather=False`` (the reference's loss is per-GPU local).
 
 GPU path: the fused exact-fp32 MFMA kernels of ``csrc/ntxent.hip`` (no N×N logits, no mask or
@@ -71,14 +73,25 @@ class _NTXentHipFn(torch.autograd.Function):
         R, D = z.shape
         dev = z.device
         zb = z.contiguous() if z.dtype == torch.bfloat16 else z.to(torch.bfloat16).contiguous()
-        zn = torch.empty((R, D), device=dev, dtype=torch.float32)
-        inv = torch.empty((R,), device=dev, dtype=torch.float32)
-        ops.nt_normalize(zb, zn, inv)
         if gather and st.comm:
-            zall = torch.empty((st.world_size * R, D), device=dev, dtype=torch.float32)
-            dist.all_gather_into_tensor(zall, zn, group=st.group)
+            # global negatives: the ranks exchange bf16 z (half the bytes of gathering fp32 ẑ)
+            # and every rank normalises all W·R rows with the same row-wise kernel, so its copy
+            # of a peer's ẑ is bitwise the peer's own.  The exchange sits between the head and the
+            # loss (nothing else in the step is independent of it); at 8 ranks it moves 8 x 256
+            # KiB, latency-bound on RCCL's launch floor
+            W = st.world_size
             col_offset = st.rank * R
+            zb_all = torch.empty((W * R, D), device=dev, dtype=torch.bfloat16)
+            dist.all_gather_into_tensor(zb_all, zb, group=st.group)
+            zall = torch.empty((W * R, D), device=dev, dtype=torch.float32)
+            inv_all = torch.empty((W * R,), device=dev, dtype=torch.float32)
+            ops.nt_normalize(zb_all, zall, inv_all)
+            zn = zall[col_offset:col_offset + R]
+            inv = inv_all[col_offset:col_offset + R]
         else:
+            zn = torch.empty((R, D), device=dev, dtype=torch.float32)
+            inv = torch.empty((R,), device=dev, dtype=torch.float32)
+            ops.nt_normalize(zb, zn, inv)
             zall = zn
             col_offset = 0
         Ccols = zall.shape[0]

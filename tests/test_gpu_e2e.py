@@ -107,3 +107,56 @@ def test_hip_graph_replay_matches_eager():
     lb = [float(b.step(x).item()) for x in xs]
     for u, v in zip(la, lb):
         assert abs(u - v) < 2e-2 * max(1.0, abs(u)), (la, lb)
+
+
+@pytest.mark.timeout(600)
+def test_golden_trajectory_resnet50_batch128_60_steps():
+    """The flagship model trains on the bf16 HIP path: ResNet-50 (CIFAR stem), batch 128, 60
+    optimizer steps (warmup + cosine, LARS) against the fp32 reference-semantics torch path
+    from identical weights and views.  Both losses must fall by >= 0.3 (measured: 5.54 -> 4.8
+    on both paths) and the trajectories must agree (bounds below)."""
+    from simclr_amd.data.datasets import synthetic_dataset
+    from simclr_amd.data.loader import ContrastiveLoader
+    from simclr_amd.config import compose, task_config, CONF_DIR
+    ov = ["experiment.base_cnn=resnet50", "experiment.batches=128", "data.synthetic=true",
+          "model.cifar_stem=true", "parameter.epochs=8", "parameter.warmup_epochs=1"]
+    cfg = task_config(compose(str(CONF_DIR), "config", ov))
+    ds = synthetic_dataset(1024, 10)
+    dev = torch.device("cuda", 0)
+    xs = []
+    for ep in range(1, 9):
+        loader = ContrastiveLoader(ds, 128, dev, seed=7)
+        loader.set_epoch(ep)
+        xs += [x.clone() for x, _ in loader]
+    xs = xs[:60]
+    assert len(xs) == 60
+
+    def trainer(precision):
+        from simclr_amd.parallel import state as pstate
+        from simclr_amd.train.pretrain import Trainer
+        pstate.reset()
+        st = pstate.get()
+        st.device = dev
+        torch.manual_seed(0)
+        return Trainer(cfg, st, len(ds), precision=precision)
+    t_hip = trainer("bf16")
+    t_ref = trainer("fp32")
+    assert t_hip.hip and not t_ref.hip
+    with torch.no_grad():
+        t_ref.store.master.copy_(t_hip.store.master)
+    l_hip = [float(t_hip.step(x).item()) for x in xs]
+    l_ref = [float(t_ref.step(x).item()) for x in xs]
+    diffs = [abs(a - b) for a, b in zip(l_hip, l_ref)]
+    print("hip", [round(v, 3) for v in l_hip])
+    print("ref", [round(v, 3) for v in l_ref])
+    print("max |d|", max(diffs), "mean |d|", sum(diffs) / len(diffs))
+    first_h, last_h = sum(l_hip[:10]) / 10, sum(l_hip[-10:]) / 10
+    first_r, last_r = sum(l_ref[:10]) / 10, sum(l_ref[-10:]) / 10
+    assert last_h < first_h - 0.3 and last_r < first_r - 0.3, (first_h, last_h, first_r, last_r)
+    # step-wise agreement while the two weight trajectories are still close (measured on MI355X:
+    # max 0.035, mean 0.014 over the first 20 steps); afterwards bf16 vs fp32 rounding makes the
+    # per-batch losses (which jump ±0.1 from batch to batch) drift apart, so the later steps are
+    # compared as 5-step running means (measured max 0.081, mean 0.032 over 60 steps)
+    assert max(diffs[:20]) < 0.06 and sum(diffs[:20]) / 20 < 0.025, diffs[:20]
+    sm = [abs(sum(l_hip[i:i + 5]) - sum(l_ref[i:i + 5])) / 5 for i in range(len(xs) - 4)]
+    assert max(sm) < 0.12 and sum(sm) / len(sm) < 0.05, sm
