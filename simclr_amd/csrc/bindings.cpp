@@ -408,12 +408,16 @@ int64_t wgrad_nsplit(std::vector<int64_t> gv, int64_t variant) {
   return wgrad_splits(geom_from(gv), (int)variant);
 }
 
+int64_t wgrad_ntiles(std::vector<int64_t> gv, int64_t variant) {
+  return wgrad_tiles(geom_from(gv), (int)variant);
+}
+
 void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tensor& out,
            std::vector<int64_t> gv, int64_t splits, int64_t creal, double beta,
            const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
            int64_t pro_seg_rows, bool pro_relu, int64_t pro_S, int64_t variant,
            const c10::optional<Tensor>& dY2, const c10::optional<Tensor>& dp_coef,
-           int64_t dp_seg_rows, int64_t dp_S) {
+           int64_t dp_seg_rows, int64_t dp_S, const c10::optional<Tensor>& tickets) {
   const ConvGeom g = geom_from(gv);
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int64_t K = (int64_t)g.KH * g.KW * g.C;
@@ -447,8 +451,15 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
     f.dp_seg_rows = (int)dp_seg_rows;
     f.dp_S = (int)dp_S;
   }
+  int* tk = nullptr;
+  if (tickets.has_value() && tickets->defined()) {
+    check_dev(*tickets, at::kInt, "tickets");
+    TORCH_CHECK(tickets->numel() >= wgrad_tiles(g, (int)variant),
+                "wgrad: tickets must hold one word per output tile");
+    tk = tickets->data_ptr<int>();
+  }
   conv_wgrad(g, bf(dY, "dY"), bf(X, "X"), (size_t)X.numel(), f32w(partial, "partial"), (int)splits,
-             f32w(out, "out"), (int)creal, (float)beta, f, (int)variant, cur_stream());
+             f32w(out, "out"), (int)creal, (float)beta, f, (int)variant, cur_stream(), tk);
 }
 
 void weight_transform(const Tensor& W, const Tensor& Wt, std::vector<int64_t> p) {
@@ -974,7 +985,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_variant_ok(int v, int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_vok);
   m.def("wgrad_variant_ok(int v, int[] geom, bool pro, bool dy_pro) -> bool", &wgrad_vok);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
-  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
+  m.def("wgrad_tiles(int[] geom, int variant=-1) -> int", &wgrad_ntiles);
+  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1, Tensor(c!)? tickets=None) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);
   m.def("weight_transform_plan(Tensor[] Ws, Tensor[] Wts, int[] p) -> Tensor", &weight_transform_plan);
   m.def("weight_transform_batch(Tensor table, int total_blocks) -> ()", &weight_transform_batch);

@@ -113,7 +113,10 @@ bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro);
 int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
                 float* partial, int splits, float* out, int Creal, float beta,
-                const ConvFusion& f, int variant, hipStream_t s);
+                const ConvFusion& f, int variant, hipStream_t s, int* tickets = nullptr);
+// output tiles of a weight-gradient launch (ticket words of the in-kernel split reduction)
+int wgrad_tiles(const ConvGeom& g, int variant);
+bool wgrad_inkernel_reduce_ok(const ConvGeom& g, int Creal);
 // one dgrad weight transform (see weight_transform_batch): Wt[ci][khs][kws][co] =
 // W[co][kh0 + khs*sh][kw0 + kws*sw][ci]; blocks [blk0, blk0 + nblk) of the batch launch
 struct WtDesc {

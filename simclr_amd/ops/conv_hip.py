@@ -156,6 +156,25 @@ def _parse_variants(spec):
 # SIMCLR_WGRAD_VARIANTS="lo-hi,...": autotune the weight gradients over these variants only
 # (attribution experiments: register-staged vs LDS-DMA tiles beside the dgrad chain)
 _WG_ONLY = _parse_variants(os.environ.get("SIMCLR_WGRAD_VARIANTS", ""))
+# split reduction inside the weight-gradient kernel (last arriver per tile, conv.hip
+# wgrad_finish) instead of separate reduce launches.  Opt-in (SIMCLR_WGRAD_INKERNEL_REDUCE=1):
+# measured 25.06 vs 23.06 ms/step (tools/envab.sh, 2 rounds) — one block per output tile reads
+# ~13 x 64 KB of slabs with ~16 KB in flight, a latency-bound serial tail on every weight
+# gradient, where the separate reduce spreads the same bytes over the whole chip
+_WG_INKERNEL = os.environ.get("SIMCLR_WGRAD_INKERNEL_REDUCE", "0") == "1"
+# zeroed, self-resetting arrival tickets per (problem, variant, stream use): launches that share
+# a buffer are ordered on one stream (a site's weight gradients) — the tuning trials and the
+# live launch use separate buffers
+_TICKETS: dict = {}
+
+
+def _tickets(ops, key, geom, v, dev, trial: bool):
+    k = (key, v, trial, dev)
+    t = _TICKETS.get(k)
+    if t is None:
+        t = torch.zeros(ops.wgrad_tiles(geom, v), device=dev, dtype=torch.int32)
+        _TICKETS[k] = t
+    return t
 
 
 def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
@@ -180,11 +199,12 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
             sps -= 1
         return dS * sps
 
-    def launch(v, o):
+    def launch(v, o, trial=False):
         splits = nsplit(v)
         partial = torch.empty((splits * N * K,), device=dY.device, dtype=torch.float32)
+        tk = _tickets(ops, key, geom, v, dY.device, trial) if _WG_INKERNEL else None
         ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v,
-                  dY2, dcoef, dseg, dS)
+                  dY2, dcoef, dseg, dS, tk)
 
     v = tuning.cached(key)
     if v is None:
@@ -193,7 +213,7 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
         if _WG_ONLY is not None:  # experiment: restrict the candidates (fallback: all)
             cands = [v for v in cands if v in _WG_ONLY] or cands
         v = tuning.pick(key, cands, 1 if N <= 64 else 0,
-                        lambda vv: launch(vv, torch.empty_like(out)))
+                        lambda vv: launch(vv, torch.empty_like(out), trial=True))
     launch(v, out)
 
 

@@ -193,6 +193,7 @@ def pretrain(cfg) -> dict:
         start_epoch = int(blob["epoch"]) + 1
         loader.counter = int(blob["step"])
     max_steps = cfg_get(cfg, "runtime.max_steps", None)
+    log_every = int(cfg_get(cfg, "runtime.log_every", 0) or 0)  # progress lines (syncs the step)
     use_graph = bool(cfg_get(cfg, "runtime.hip_graph", False)) and tr.hip
     metrics = MetricsWriter("metrics.jsonl" if rank == 0 else None)
     save_every = cfg["experiment"]["save_model_epoch"]
@@ -220,6 +221,8 @@ def pretrain(cfg) -> dict:
             loss = tr.step(x)
             nsteps += 1
             step_global += 1
+            if log_every and rank == 0 and step_global % log_every == 0:
+                log.info("step %d loss %.4f", step_global, float(loss))
             if prof is not None and step_global >= prof_win[1]:
                 _stop_profiler(prof, rank)
                 prof = None

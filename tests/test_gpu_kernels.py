@@ -482,3 +482,48 @@ def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
             out = torch.empty(Co, k, k, C, device=DEV)
             ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, None, None, 0, False, 1, v)
             assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)
+
+
+@pytest.mark.parametrize("k,s,p,C,Co,H", [(1, 1, 0, 64, 256, 16), (3, 1, 1, 64, 64, 16),
+                                           (3, 2, 1, 128, 192, 16), (3, 1, 1, 64, 64, 32),
+                                           (3, 1, 1, 256, 512, 4), (3, 1, 1, 64, 64, 5),
+                                           (1, 1, 0, 256, 64, 32)])
+def test_wgrad_inkernel_split_reduce_every_variant(ops, k, s, p, C, Co, H):
+    """In-launch split reduction (conv.hip wgrad_finish: last arriver per tile sums the slabs in
+    split order): every admissible variant and split counts 1 / 3 / default / 40 (> the
+    two-level threshold of the separate reduce) against torch's fp32 weight gradient and the
+    separate-reduce path; the self-resetting tickets are reused across launches."""
+    from simclr_amd.ops.conv_hip import fwd_geom
+    torch.manual_seed(17)
+    N = 8
+    x = _bf(torch.randn(N, C, H, H, device=DEV))
+    wr = (_bf(torch.randn(Co, C, k, k, device=DEV)) * 0.05).float().requires_grad_(True)
+    y = F.conv2d(x.float(), wr, None, s, p)
+    gy = _bf(torch.randn_like(y))
+    y.backward(gy.float())
+    OH, OW = y.shape[-2:]
+    g = fwd_geom(N, H, H, C, OH, OW, k, k, s, p, Co)
+    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    K = k * k * C
+    M = N * OH * OW
+    vs = [v for v in range(ops.wgrad_nvariants()) if ops.wgrad_variant_ok(v, g, False, False)]
+    assert vs
+    for v in vs:
+        iters = M // 256 if v >= 17 else (M + 63) // 64
+        tk = torch.zeros(ops.wgrad_tiles(g, v), device=DEV, dtype=torch.int32)
+        for splits in sorted({1, 3, ops.wgrad_splits(g, v), min(40, iters)}):
+            part = torch.empty(splits * Co * K, device=DEV)
+            a = torch.full((Co, k, k, C), float("nan"), device=DEV)
+            b = torch.empty(Co, k, k, C, device=DEV)
+            for _ in range(2):  # second launch: tickets were reset by the first
+                ops.wgrad(dyn, xn, part, a, g, splits, C, 0.0, None, None, 0, False, 1, v,
+                          None, None, 0, 1, tk)
+            ops.wgrad(dyn, xn, part, b, g, splits, C, 0.0, None, None, 0, False, 1, v)
+            assert int(tk.abs().sum()) == 0, (v, splits)
+            assert torch.isfinite(a).all(), (v, splits)
+            if splits <= 32:  # same slab_sum4 order as the one-level separate reduce: bitwise
+                assert torch.equal(a, b), (v, splits)
+            else:  # the separate reduce sums in groups of 16 first: fp32 reassociation only
+                assert _rel(a, b) < 1e-6, (v, splits, _rel(a, b))
+            assert _rel(a.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)

@@ -9,7 +9,7 @@ root=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$root/gpurun_out/e2e_diag
 rm -rf "$out"; mkdir -p "$out"
 DATA="data.synthetic=true data.synthetic_size=50000 data.synthetic_colour=false data.synthetic_noise=90 experiment.base_cnn=resnet18 $*"
-for be in hip torch; do
+for be in ${BACKENDS:-hip torch}; do
   run=${TMPDIR:-/tmp}/simclr_diag_$be
   rm -rf "$run"; mkdir -p "$run/run"
   timeout -k 10 120 python - <<PY || exit $?
@@ -21,10 +21,14 @@ m = ContrastiveModel("resnet18")
 torch.save({"module." + k: v for k, v in m.state_dict().items()}, "$run/run/epoch=0-cifar10.pt")
 PY
   prec=bf16; [ $be = torch ] && prec=fp32
+  # the stock torch path's MIOpen convolutions: heuristic solver choice (an exhaustive find per
+  # new shape takes minutes on the first step)
+  export MIOPEN_FIND_MODE=FAST
   echo "pretrain $be $E epochs"
   timeout -k 10 1200 python main.py $DATA runtime.backend=$be runtime.precision=$prec \
     experiment.batches=512 parameter.epochs=$E parameter.warmup_epochs=2 \
-    experiment.save_model_epoch=$E hydra.run.dir=$run/run > "$out/pretrain_$be.log" 2>&1 || exit $?
+    experiment.save_model_epoch=$E runtime.log_every=25 hydra.run.dir=$run/run \
+    > "$out/pretrain_$be.log" 2>&1 || exit $?
   tail -2 "$out/pretrain_$be.log"; cp "$run/run/metrics.jsonl" "$out/metrics_$be.jsonl"
   echo "probe diag $be"
   timeout -k 10 900 python tools/probe_diag.py "$run/run" $DATA runtime.backend=$be \
