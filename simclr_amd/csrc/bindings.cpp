@@ -462,6 +462,44 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
              f32w(out, "out"), (int)creal, (float)beta, f, (int)variant, cur_stream(), tk);
 }
 
+
+// fused 1x1 backward of a bottleneck conv3 (conv.hip conv1x1_bwd_dual): returns nothing; writes
+// gm [M][Ci], stats [S*bps][2][Ci] (BN2-backward partials), wpart [S*bps][Co][Ci] (dW slabs)
+void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
+                         const c10::optional<Tensor>& coef, const Tensor& X, const Tensor& xss,
+                         const Tensor& xmi, const Tensor& Wt, const Tensor& gm,
+                         const Tensor& stats, const Tensor& wpart, int64_t S, int64_t bps) {
+  const int64_t CI = gm.size(-1);
+  const int64_t M = gm.numel() / CI;
+  const int64_t CO = G.numel() / M;
+  TORCH_CHECK(CO == 256 && CI == 64, "conv1x1_bwd_dual: Co = 256, Ci = 64 only");
+  TORCH_CHECK(G.numel() == M * CO && X.numel() == M * CI && Wt.numel() == CI * CO,
+              "conv1x1_bwd_dual: operand sizes");
+  TORCH_CHECK(S >= 1 && S <= 2 && bps >= 1 && M % S == 0 && (M / S) % (64 * bps) == 0,
+              "conv1x1_bwd_dual: every block's rows must lie in one segment (64-row tiles)");
+  TORCH_CHECK(xss.numel() >= 2 * S * CI && xmi.numel() >= 2 * S * CI, "conv1x1_bwd_dual: BN2 tables");
+  TORCH_CHECK(stats.numel() >= S * bps * 2 * CI, "conv1x1_bwd_dual: stats size");
+  TORCH_CHECK(wpart.numel() >= S * bps * CO * CI, "conv1x1_bwd_dual: wpart size");
+  TORCH_CHECK(M * CO * 2 < (int64_t(1) << 31), "conv1x1_bwd_dual: 32-bit buffer offsets");
+  const uint16_t* a3 = optbf(A3, "A3");
+  const float* cf = optf32(coef, "coef");
+  if (a3 != nullptr) {
+    TORCH_CHECK(A3->numel() == G.numel() && cf != nullptr && coef->numel() >= 3 * S * CO,
+                "conv1x1_bwd_dual: lazy BN-backward needs A3 [M][Co] and coef [3][S][Co]");
+  }
+  conv1x1_bwd_dual(bf(G, "G"), a3, cf, bf(X, "X"), f32(xss, "xss"), f32(xmi, "xmi"),
+                   bf(Wt, "Wt"), bfw(gm, "gm"), f32w(stats, "stats"), f32w(wpart, "wpart"),
+                   (int)M, (int)CO, (int)CI, (int)S, (int)bps, cur_stream());
+}
+
+void wgrad_reduce_slabs_op(const Tensor& partial, int64_t splits, const Tensor& out, double beta) {
+  const int64_t n = out.numel();
+  TORCH_CHECK(n % 4 == 0 && partial.numel() >= splits * n && splits >= 1,
+              "wgrad_reduce_slabs: sizes");
+  wgrad_reduce_slabs(f32w(partial, "partial"), (int)splits, f32w(out, "out"), (size_t)n,
+                     (float)beta, cur_stream());
+}
+
 void weight_transform(const Tensor& W, const Tensor& Wt, std::vector<int64_t> p) {
   TORCH_CHECK(p.size() == 10, "weight_transform params");
   const int Co = p[0], KH = p[1], KW = p[2], Ci = p[3], KHs = p[4], KWs = p[5];
@@ -986,6 +1024,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("wgrad_variant_ok(int v, int[] geom, bool pro, bool dy_pro) -> bool", &wgrad_vok);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad_tiles(int[] geom, int variant=-1) -> int", &wgrad_ntiles);
+  m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor xss, Tensor xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps) -> ()", &conv1x1_bwd_dual_op);
+  m.def("wgrad_reduce_slabs(Tensor(a!) partial, int splits, Tensor(b!) out, float beta=0.0) -> ()", &wgrad_reduce_slabs_op);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1, Tensor(c!)? tickets=None) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);
   m.def("weight_transform_plan(Tensor[] Ws, Tensor[] Wts, int[] p) -> Tensor", &weight_transform_plan);

@@ -2252,6 +2252,229 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 
+
+// -------------------------------------------------- fused 1x1 backward: dgrad + wgrad in one pass
+// A bottleneck's conv3 backward at 32x32 (ResNet-50 layer1: Ci = 64, Co = 256, M = 2^20 rows) is
+// HBM-bound on its output gradient: the dgrad reads dY (or g and the pre-BN activation when the
+// BN3 backward runs in its prologue: 1 GB), and the weight gradient re-reads the same 1 GB on the
+// side stream (r2: 171-235 TF/s, 4.7 ms of weight-gradient wall time per step).  This kernel
+// reads every operand once: a persistent block walks its m-tiles (64 rows) of one view segment,
+// forms the dY tile (BN-backward prologue in registers) and the X tile (BN2-apply + ReLU) in LDS,
+// and per tile
+//   dX[64 x Ci]  = dY[64 x Co] · W[Co x Ci]     (Wᵀ resident in LDS; dY read non-transposed)
+//   dW[Co x Ci] += dYᵀ[Co x 64] · X[64 x Ci]    (both read with ds_read_b64_tr_b16, registers)
+// with the dgrad's mode-3 epilogue (ReLU mask of BN2 from the raw a2 tile, Σg / Σg·x̂ partials of
+// the BN2 backward).  At the end each block writes its dW slab (summed by the split reduction)
+// and one partial-statistics row.  Reference math: /root/reference/model.py Bottleneck conv3 +
+// SyncBatchNorm backward.
+struct Dual1x1Args {
+  const uint16_t* G;     // [M][CO]: dY, or the BN3-backward input g (lazy)
+  const uint16_t* A3;    // [M][CO] pre-BN activation for the lazy form, or nullptr
+  const float* coef;     // [3][S][CO] lazy BN-backward coefficients
+  const uint16_t* X;     // [M][CI] pre-BN a2 (conv3's forward input before BN2 + ReLU)
+  const float* xss;      // [2][S][CI] BN2 scale / shift
+  const float* xmi;      // [2][S][CI] BN2 mean / invstd
+  const uint16_t* Wt;    // [CI][CO] dgrad weight (transformed OHWI, 1x1)
+  uint16_t* gm;          // [M][CI] masked input gradient
+  float* stats;          // [S * bps][2][CI] partials Σg, Σg·x̂
+  float* wpart;          // [S * bps][CO][CI] dW slabs
+  int M, S, seg_rows, bps, tiles_per_block;
+  uint32_t g_bytes, x_bytes;
+};
+
+template <int CO, int CI>
+__global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
+  static_assert(CO == 256 && CI == 64, "tile mapping written for Co = 256, Ci = 64");
+  constexpr int BMT = 64;  // rows per m-tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ds = (uint16_t*)smem;             // [2][64][CO]  tr_swz<CO> image of dY
+  uint16_t* Xs = Ds + 2 * BMT * CO;           // [2][64][CI]  tr_swz<CI> image of relu(bn2(a2))
+  uint16_t* Xr = Xs + 2 * BMT * CI;           // [2][64][CI]  raw a2 (epilogue mask / x̂)
+  uint16_t* Ws = Xr + 2 * BMT * CI;           // [CI][CO]     Wᵀ, chunk ^= row & 7
+  float* red = (float*)(Ws + CI * CO);        // [4][CI][2]   statistics reduction
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int seg = blk / p.bps;
+  const int mbeg = seg * p.seg_rows + (blk - seg * p.bps) * p.tiles_per_block * BMT;
+  const int T = p.tiles_per_block;
+  const bool lazy = p.A3 != nullptr;
+
+  const __amdgpu_buffer_rsrc_t rg =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.G, (short)0, (int)p.g_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(lazy ? p.A3 : p.G), (short)0, (int)p.g_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
+
+  // W^T resident for the whole block (one 32 KB read per block)
+  for (int c = tid; c < CI * CO / 8; c += 256) {
+    const int row = c / (CO / 8), ch = c % (CO / 8);
+    *(u32x4*)(Ws + row * CO + ((ch ^ (row & 7)) * 8)) = *(const u32x4*)(p.Wt + (size_t)c * 8);
+  }
+
+  // loader mapping: dY chunk column fixed per thread (8 output channels), rows tid/32 + 8j;
+  // X chunk column fixed (8 input channels), rows tid/8 + 32j
+  constexpr int GCH = CO / 8, XCH = CI / 8;
+  const int gch = tid % GCH, grow = tid / GCH;  // rows grow + 8j, j < 8
+  const int xch = tid % XCH, xrow = tid / XCH;  // rows xrow + 32j, j < 2
+  float cA[8], cB[8], cD[8], xsc[8], xsh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int co = gch * 8 + e, ci = xch * 8 + e;
+    cA[e] = lazy ? p.coef[seg * CO + co] : 1.f;
+    cB[e] = lazy ? p.coef[(p.S + seg) * CO + co] : 0.f;
+    cD[e] = lazy ? p.coef[(2 * p.S + seg) * CO + co] : 0.f;
+    xsc[e] = p.xss[seg * CI + ci];
+    xsh[e] = p.xss[(p.S + seg) * CI + ci];
+  }
+  // epilogue tables of the lane's 16 channels: ci = fn*16 + 4g + r
+  float esc[4][4], esh[4][4], emu[4][4], einv[4][4];
+#pragma unroll
+  for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ci = fn * 16 + 4 * g + r;
+      esc[fn][r] = p.xss[seg * CI + ci];
+      esh[fn][r] = p.xss[(p.S + seg) * CI + ci];
+      emu[fn][r] = p.xmi[seg * CI + ci];
+      einv[fn][r] = p.xmi[(p.S + seg) * CI + ci];
+    }
+
+  u32x4 rG[8], rA[8], rX[2];
+  auto gload = [&](int t) {
+    const int m0 = mbeg + t * BMT;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t off = (uint32_t)(((size_t)(m0 + grow + 8 * j) * CO + gch * 8) * 2);
+      rG[j] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
+      if (lazy) rA[j] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      rX[j] = __builtin_amdgcn_raw_buffer_load_b128(
+          rx, (uint32_t)(((size_t)(m0 + xrow + 32 * j) * CI + xch * 8) * 2), 0, 0);
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = grow + 8 * j;
+      *(u32x4*)(Ds + buf * BMT * CO + r * CO + tr_swz<CO>(r, gch * 8)) =
+          lazy ? bnbwd8(rG[j], rA[j], cA, cB, cD, true) : rG[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = xrow + 32 * j;
+      *(u32x4*)(Xs + buf * BMT * CI + r * CI + tr_swz<CI>(r, xch * 8)) =
+          affine_relu8(rX[j], xsc, xsh, true, true);
+      *(u32x4*)(Xr + buf * BMT * CI + r * CI + xch * 8) = rX[j];
+    }
+  };
+
+  f32x4 accw[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float s1[4][4], s2[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { s1[i][j] = 0.f; s2[i][j] = 0.f; }
+
+  if (T > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < T) gload(t + 1);
+    const uint16_t* Db = Ds + cur * BMT * CO;
+    // dgrad: D[ci][m] over k = co; wave owns rows m = wid*16 + li
+    f32x4 accd[4];
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) accd[fn] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int mrow = wid * 16 + li;
+#pragma unroll
+    for (int ks = 0; ks < CO / 32; ++ks) {
+      const int lch = ks * 4 + g;
+      const bf16x8 bfr = *(const bf16x8*)(Db + mrow * CO + tr_swz<CO>(mrow, lch * 8));
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        const int wr = fn * 16 + li;
+        const bf16x8 af = *(const bf16x8*)(Ws + wr * CO + ((lch ^ (wr & 7)) * 8));
+        accd[fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, accd[fn], 0, 0, 0);
+      }
+    }
+    // wgrad: accw[fm][fn] += dY^T · X  (wave owns co = wid*64 .. +64)
+    wgrad_mma<CO, CI, 4, 1>(Db, Xs + cur * BMT * CI, accw);
+    // mode-3 epilogue: g = [bn2(a2) > 0] · round(dX), Σg, Σg·x̂
+    const int m = mbeg + t * BMT + mrow;
+    const uint16_t* xr = Xr + cur * BMT * CI + mrow * CI;
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      const int ci = fn * 16 + 4 * g;
+      const u32x2 yv = *(const u32x2*)(xr + ci);
+      const float y[4] = {lo_bf(yv.x), hi_bf(yv.x), lo_bf(yv.y), hi_bf(yv.y)};
+      float gv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = bf2f(f2bf(accd[fn][r]));
+        gv[r] = y[r] * esc[fn][r] + esh[fn][r] > 0.f ? a : 0.f;
+        s1[fn][r] += gv[r];
+        s2[fn][r] += gv[r] * ((y[r] - emu[fn][r]) * einv[fn][r]);
+      }
+      const u32x2 w = {pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
+      __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CI + ci));
+    }
+    if (t + 1 < T) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  // dW slab of this block: [co][ci]
+  float* wp = p.wpart + (size_t)blk * CO * CI;
+#pragma unroll
+  for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        wp[(size_t)(wid * 64 + fm * 16 + g * 4 + i) * CI + fn * 16 + li] = accw[fm][fn][i];
+  // statistics: lanes sharing channels (same g) sum over li, then the 4 waves through LDS
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[fn][r] += __shfl_xor(s1[fn][r], off, 64);
+        s2[fn][r] += __shfl_xor(s2[fn][r], off, 64);
+      }
+  if (li == 0) {
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ci = fn * 16 + 4 * g + r;
+        red[(wid * CI + ci) * 2 + 0] = s1[fn][r];
+        red[(wid * CI + ci) * 2 + 1] = s2[fn][r];
+      }
+  }
+  __syncthreads();
+  if (tid < CI) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      a += red[(w * CI + tid) * 2 + 0];
+      b += red[(w * CI + tid) * 2 + 1];
+    }
+    p.stats[((size_t)blk * 2 + 0) * CI + tid] = a;
+    p.stats[((size_t)blk * 2 + 1) * CI + tid] = b;
+  }
+}
+
 }  // namespace
 
 void conv_weight_transform_batch(const WtDesc* d, int n, int total_blocks, hipStream_t s) {
@@ -2533,5 +2756,55 @@ void conv_weight_transform(const uint16_t* W, uint16_t* Wt, int Co, int KH, int 
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(weight_transform, dim3(blocks), dim3(256), 0, s, W, Wt, Co, KH, KW, Ci, KHs,
                      KWs, kh0, sh, kw0, sw);
+  HIP_CHECK_LAUNCH();
+}
+
+size_t conv1x1_bwd_dual_lds() {
+  return (size_t)2 * 64 * 256 * 2 + 2 * (size_t)2 * 64 * 64 * 2 + (size_t)64 * 256 * 2 +
+         (size_t)4 * 64 * 2 * 4;
+}
+
+void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, const uint16_t* X,
+                      const float* xss, const float* xmi, const uint16_t* Wt, uint16_t* gm,
+                      float* stats, float* wpart, int M, int CO, int CI, int S, int bps,
+                      hipStream_t s) {
+  Dual1x1Args a{};
+  a.G = G; a.A3 = A3; a.coef = coef; a.X = X; a.xss = xss; a.xmi = xmi; a.Wt = Wt; a.gm = gm;
+  a.stats = stats; a.wpart = wpart;
+  a.M = M; a.S = S; a.seg_rows = M / S; a.bps = bps;
+  a.tiles_per_block = a.seg_rows / 64 / bps;
+  a.g_bytes = (uint32_t)((size_t)M * CO * 2);
+  a.x_bytes = (uint32_t)((size_t)M * CI * 2);
+  const size_t lds = conv1x1_bwd_dual_lds();
+  if (CO == 256 && CI == 64) {
+    hipLaunchKernelGGL((conv1x1_bwd_dual<256, 64>), dim3(S * bps), dim3(256), lds, s, a);
+  } else {
+    fprintf(stderr, "conv1x1_bwd_dual: unsupported Co=%d Ci=%d\n", CO, CI);
+    abort();  // the bindings reject this
+  }
+  HIP_CHECK_LAUNCH();
+}
+
+// out[n4] (+)= Σ_s slabs (the separate split reduction of conv_wgrad, for producers that write
+// [splits][N*K] fp32 slabs themselves)
+void wgrad_reduce_slabs(float* partial, int splits, float* out, size_t n, float beta,
+                        hipStream_t s) {
+  const size_t n4 = n / 4;
+  int sstride = 1, count = splits;
+  constexpr int GROUP = 16;
+  if (splits > 2 * GROUP) {
+    const int G = (splits + GROUP - 1) / GROUP;
+    int bx = (int)((n4 + 255) / 256);
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(wgrad_reduce_l1, dim3(bx, G), dim3(256), 0, s, (float4*)partial, splits,
+                       GROUP, n4);
+    HIP_CHECK_LAUNCH();
+    sstride = GROUP;
+    count = G;
+  }
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(wgrad_reduce_vec4, dim3(blocks), dim3(256), 0, s, (const float4*)partial,
+                     (float4*)out, count, sstride, n4, beta);
   HIP_CHECK_LAUNCH();
 }

@@ -114,6 +114,14 @@ int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
                 float* partial, int splits, float* out, int Creal, float beta,
                 const ConvFusion& f, int variant, hipStream_t s, int* tickets = nullptr);
+// fused 1x1 backward (dgrad + wgrad + BN2-backward partials in one pass, Co = 256, Ci = 64)
+size_t conv1x1_bwd_dual_lds();
+void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, const uint16_t* X,
+                      const float* xss, const float* xmi, const uint16_t* Wt, uint16_t* gm,
+                      float* stats, float* wpart, int M, int CO, int CI, int S, int bps,
+                      hipStream_t s);
+void wgrad_reduce_slabs(float* partial, int splits, float* out, size_t n, float beta,
+                        hipStream_t s);
 // output tiles of a weight-gradient launch (ticket words of the in-kernel split reduction)
 int wgrad_tiles(const ConvGeom& g, int variant);
 bool wgrad_inkernel_reduce_ok(const ConvGeom& g, int Creal);

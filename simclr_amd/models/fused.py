@@ -174,6 +174,10 @@ class FusedStages:
         # two-level pass over one row per row-block.  Off by default: measured neutral (24.10 vs
         # 24.07 ms/step — the reduce launch's cost is its dispatch, not its reads) and atomic
         # order is not reproducible; deterministic runs never use it.
+        # a bottleneck's conv3 backward at Ci = 64 / Co = 256 (ResNet-50 layer1) as ONE fused
+        # pass (conv.hip conv1x1_bwd_dual): dgrad + BN2 mask / partials + weight gradient, so the
+        # 0.5-1 GB output gradient is read once instead of once per pass
+        self.dual_1x1 = os.environ.get("SIMCLR_DUAL_1X1", "1") != "0"
         g = os.environ.get("SIMCLR_STATS_GROUPS", "0")
         self.stats_groups = int(g) if g.isdigit() else 0
         self._accs = {}
@@ -483,6 +487,58 @@ class FusedStages:
         side.wait_stream(torch.cuda.current_stream(dyn.device))
         with torch.cuda.stream(side):
             run()
+
+    @staticmethod
+    def _dual_bps(rows_seg: int) -> int:
+        """Persistent blocks per view segment of conv1x1_bwd_dual (64-row tiles, equal shares)."""
+        tiles = rows_seg // 64
+        b = min(128, tiles)
+        while b > 1 and tiles % b:
+            b -= 1
+        return b
+
+    def _dual_ok(self, cs: _ConvSpec, dyn: torch.Tensor, xin: torch.Tensor, pro_ss, a_prev,
+                 S: int) -> bool:
+        M = dyn.numel() // dyn.shape[-1]
+        return (getattr(self, "dual_1x1", False) and cs.k == 1 and cs.stride == 1
+                and cs.conv.out_channels == 256 and cs.conv.in_channels == 64
+                and xin is a_prev and pro_ss is not None and self._groups() == 0
+                and M % S == 0 and (M // S) % 64 == 0 and M * 256 * 2 < (1 << 31))
+
+    def _dual_backward(self, ops, dyn, bnb, cs: _ConvSpec, a_prev, bs_prev: _BNState, S: int):
+        """conv3 dgrad (mode-3 epilogue of BN2) + weight gradient in one launch; the weight
+        gradient's split reduction runs on the side stream.  Returns (gm, partials, blocks per
+        segment) like ``_dgrad`` with ``bn_epi=("mask", ...)``."""
+        Nb, H, W, Ci = a_prev.shape
+        Co = cs.conv.out_channels
+        M = Nb * H * W
+        bps = self._dual_bps(M // S)
+        w = shadow_ohwi(cs.conv.weight, Ci)
+        wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
+        dev = dyn.device
+        gm = _empty_nhwc(Nb, H, W, Ci, dev)
+        stats = torch.empty((S * bps * 2 * Ci,), device=dev, dtype=torch.float32)
+        wpart = torch.empty((S * bps * Co * Ci,), device=dev, dtype=torch.float32)
+        a3, coef = (bnb[0], bnb[1]) if bnb is not None else (None, None)
+        ops.conv1x1_bwd_dual(dyn, a3, coef, a_prev, bs_prev.ss.view(-1), bs_prev.mi.view(-1), wt,
+                             gm, stats, wpart, S, bps)
+
+        def run():
+            if _SKIP_WGRAD:
+                _deliver_grad(cs.conv.weight, lambda out: None)
+                return
+            _deliver_grad(cs.conv.weight,
+                          lambda out: ops.wgrad_reduce_slabs(wpart, S * bps, out))
+
+        side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
+        if side is None:
+            run()
+        else:
+            self._side_keep.append(wpart)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                run()
+        return gm, stats, bps
 
     def _bnb_ok(self, cs: _ConvSpec, a: torch.Tensor, S: int) -> bool:
         """The BN-backward operand prologue applies to a 1x1 stride-1 conv whose per-segment
@@ -914,13 +970,18 @@ class FusedStages:
             a_prev, bs_prev = tp.acts[i - 1], tp.bns[i - 1]
             _ext.TAG = f"{b.name} conv{i + 1} dgrad"
             dyn, bnb = (g3, lazy) if (i == L and lazy is not None) else (da, None)
-            gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,
-                                       bn_epi=("mask", a_prev, bs_prev), bnb=bnb,
-                                       tail_bn=(b.convs[i - 1].bn, bs_prev, st),
-                                       acc_keys=((id(b.convs[i - 1].bn), "bwd"), None))
-            h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
-            _ext.TAG = f"{b.name} conv{i + 1} wgrad"
-            self._wgrad(ops, dyn, xin, cs, pro_ss, S, bnb=bnb)
+            if self._dual_ok(cs, dyn, xin, pro_ss, a_prev, S):
+                _ext.TAG = f"{b.name} conv{i + 1} dgrad+wgrad"
+                gm, part, nb = self._dual_backward(ops, dyn, bnb, cs, a_prev, bs_prev, S)
+                h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
+            else:
+                gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,
+                                           bn_epi=("mask", a_prev, bs_prev), bnb=bnb,
+                                           tail_bn=(b.convs[i - 1].bn, bs_prev, st),
+                                           acc_keys=((id(b.convs[i - 1].bn), "bwd"), None))
+                h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
+                _ext.TAG = f"{b.name} conv{i + 1} wgrad"
+                self._wgrad(ops, dyn, xin, cs, pro_ss, S, bnb=bnb)
             _ext.TAG = f"{b.name} bn{i} bwd"
             coef = self._bn_bwd_finish(ops, h, S)
             da_next = torch.empty_like(a_prev)

@@ -22,14 +22,20 @@ def cfg_get(cfg, dotted: str, default: Any = None) -> Any:
 
 
 def seed_everything(seed: int, deterministic: bool = False) -> None:
-    """Reference seeding (main.py:146-151): numpy + torch + all GPUs, same seed on every rank."""
+    """Reference seeding (main.py:146-151): numpy + torch + all GPUs, same seed on every rank.
+
+    The reference also sets ``cudnn.deterministic = True``; on ROCm that flag selects MIOpen's
+    deterministic convolution solvers, which run the stock-op (``runtime.backend=torch``)
+    ResNet-18 step in 12.2 s instead of 85 ms (tools/torch_step_probe.py on MI355X), so it is set
+    only with ``runtime.deterministic=true``.  The HIP kernels never use MIOpen; their
+    determinism switch is the fixed-tile policy (``ops.tuning.set_enabled(False)``)."""
     random.seed(seed)
     np.random.seed(seed)
     torch.manual_seed(seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
-    torch.backends.cudnn.deterministic = True
     torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.deterministic = bool(deterministic)
     if deterministic:
         torch.use_deterministic_algorithms(True, warn_only=True)
 

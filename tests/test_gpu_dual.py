@@ -1,0 +1,68 @@
+"""Fused 1x1 backward (csrc/conv.hip conv1x1_bwd_dual): a bottleneck conv3's dgrad (with the BN2
+ReLU-mask epilogue and the BN2-backward Σg / Σg·x̂ partials) and its weight gradient from ONE
+pass over the output gradient, with and without the lazy BN3-backward prologue
+(dY = A·g + B·a3 + D per view segment), against an fp32 PyTorch reference of the same math
+(/root/reference/model.py Bottleneck.conv3 under SyncBatchNorm)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+@pytest.mark.parametrize("Nb,H,lazy,bps", [(64, 8, True, 32), (64, 8, False, 16),
+                                           (32, 32, True, 128), (32, 32, False, 64)])
+def test_conv1x1_bwd_dual_matches_fp32(Nb, H, lazy, bps):
+    from simclr_amd.ops import _ext
+    ops = _ext.ops()
+    torch.manual_seed(Nb + H + int(lazy))
+    S, Co, Ci = 2, 256, 64
+    M = Nb * H * H
+    seg = M // S
+    G = _bf(torch.randn(M, Co, device=DEV))
+    A3 = _bf(torch.randn(M, Co, device=DEV)) if lazy else None
+    coef = torch.randn(3, S, Co, device=DEV) * 0.5 if lazy else None
+    X = _bf(torch.randn(M, Ci, device=DEV))
+    ss = torch.stack([0.5 + torch.rand(S, Ci, device=DEV), torch.randn(S, Ci, device=DEV) * 0.3])
+    mi = torch.stack([torch.randn(S, Ci, device=DEV) * 0.1, 0.5 + torch.rand(S, Ci, device=DEV)])
+    W = _bf(torch.randn(Co, Ci, device=DEV) * 0.06)        # conv3 weight [Co][Ci] (1x1)
+    Wt = W.t().contiguous()                                 # dgrad operand [Ci][Co]
+    gm = torch.empty(M, Ci, device=DEV, dtype=torch.bfloat16)
+    stats = torch.empty(S * bps * 2 * Ci, device=DEV)
+    wpart = torch.empty(S * bps * Co * Ci, device=DEV)
+    ops.conv1x1_bwd_dual(G, A3, coef.reshape(-1) if lazy else None, X, ss.reshape(-1),
+                         mi.reshape(-1), Wt, gm, stats, wpart, S, bps)
+    dW = torch.empty(Co, Ci, device=DEV)
+    ops.wgrad_reduce_slabs(wpart, S * bps, dW)
+    torch.cuda.synchronize()
+
+    # fp32 reference (operands rounded to bf16 where the kernel rounds them)
+    sg = torch.arange(M, device=DEV) // seg
+    if lazy:
+        dY = _bf(coef[0][sg] * G.float() + coef[1][sg] * A3.float() + coef[2][sg]).float()
+    else:
+        dY = G.float()
+    Xf = X.float()
+    Xp = _bf(torch.relu(Xf * ss[0][sg] + ss[1][sg])).float()
+    dX = _bf(dY @ W.float()).float()
+    mask = (Xf * ss[0][sg] + ss[1][sg]) > 0
+    g = torch.where(mask, dX, torch.zeros_like(dX))
+    xh = (Xf - mi[0][sg]) * mi[1][sg]
+    st = stats.view(S, bps, 2, Ci).sum(1)
+    ref_s1 = torch.stack([g[sg == s].sum(0) for s in range(S)])
+    ref_s2 = torch.stack([(g * xh)[sg == s].sum(0) for s in range(S)])
+    dW_ref = dY.t() @ Xp
+    assert _rel(gm, g) < 1e-2, _rel(gm, g)
+    # masks agree exactly: every zero of the reference is a zero of the kernel
+    assert int(((gm.float() != 0) & ~mask).sum()) == 0
+    assert _rel(st[:, 0], ref_s1) < 2e-3, _rel(st[:, 0], ref_s1)
+    assert _rel(st[:, 1], ref_s2) < 2e-3, _rel(st[:, 1], ref_s2)
+    assert _rel(dW, dW_ref) < 2e-3, _rel(dW, dW_ref)

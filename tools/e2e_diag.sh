@@ -21,9 +21,9 @@ m = ContrastiveModel("resnet18")
 torch.save({"module." + k: v for k, v in m.state_dict().items()}, "$run/run/epoch=0-cifar10.pt")
 PY
   prec=bf16; [ $be = torch ] && prec=fp32
-  # the stock torch path's MIOpen convolutions: heuristic solver choice (an exhaustive find per
-  # new shape takes minutes on the first step)
-  export MIOPEN_FIND_MODE=FAST
+  # (the torch path's MIOpen convolutions keep the default find mode: ~45 s of solver search on
+  # the first step, then 85 ms/step; MIOPEN_FIND_MODE=FAST from an empty find-db picks solvers
+  # that run 1.26 s/step — profiles/r3_optimization_log.md)
   echo "pretrain $be $E epochs"
   timeout -k 10 1200 python main.py $DATA runtime.backend=$be runtime.precision=$prec \
     experiment.batches=512 parameter.epochs=$E parameter.warmup_epochs=2 \
