@@ -118,6 +118,9 @@ class _BlockTape:
     mask: Optional[torch.Tensor] = None  # uint8 ReLU bitmask of ``out`` (bit per channel)
 
 
+# persistent blocks per view segment of the fused 1x1 backward (2 segments: 2x this many blocks)
+_BWD1X1_BPS = int(os.environ.get("SIMCLR_BWD1X1_BPS", "128"))
+
 # bit 8 of the igemm epilogue mode: the residual operand is stride-2 subsampled (conv.hip)
 _EPI_SUB = 256
 
@@ -177,7 +180,7 @@ class FusedStages:
         # a bottleneck's conv3 backward at Ci = 64 / Co = 256 (ResNet-50 layer1) as ONE fused
         # pass (conv.hip conv1x1_bwd_dual): dgrad + BN2 mask / partials + weight gradient, so the
         # 0.5-1 GB output gradient is read once instead of once per pass
-        self.dual_1x1 = os.environ.get("SIMCLR_DUAL_1X1", "1") != "0"
+        self.fused_bwd1x1 = os.environ.get("SIMCLR_FUSED_BWD1X1", "1") != "0"
         g = os.environ.get("SIMCLR_STATS_GROUPS", "0")
         self.stats_groups = int(g) if g.isdigit() else 0
         self._accs = {}
@@ -489,30 +492,30 @@ class FusedStages:
             run()
 
     @staticmethod
-    def _dual_bps(rows_seg: int) -> int:
+    def _bwd1x1_bps(rows_seg: int) -> int:
         """Persistent blocks per view segment of conv1x1_bwd_dual (64-row tiles, equal shares)."""
         tiles = rows_seg // 64
-        b = min(128, tiles)
+        b = min(_BWD1X1_BPS, tiles)
         while b > 1 and tiles % b:
             b -= 1
         return b
 
-    def _dual_ok(self, cs: _ConvSpec, dyn: torch.Tensor, xin: torch.Tensor, pro_ss, a_prev,
-                 S: int) -> bool:
+    def _bwd1x1_ok(self, cs: _ConvSpec, dyn: torch.Tensor, xin: torch.Tensor, pro_ss, a_prev,
+                   S: int) -> bool:
         M = dyn.numel() // dyn.shape[-1]
-        return (getattr(self, "dual_1x1", False) and cs.k == 1 and cs.stride == 1
+        return (getattr(self, "fused_bwd1x1", False) and cs.k == 1 and cs.stride == 1
                 and cs.conv.out_channels == 256 and cs.conv.in_channels == 64
                 and xin is a_prev and pro_ss is not None and self._groups() == 0
                 and M % S == 0 and (M // S) % 64 == 0 and M * 256 * 2 < (1 << 31))
 
-    def _dual_backward(self, ops, dyn, bnb, cs: _ConvSpec, a_prev, bs_prev: _BNState, S: int):
+    def _bwd1x1_fused(self, ops, dyn, bnb, cs: _ConvSpec, a_prev, bs_prev: _BNState, S: int):
         """conv3 dgrad (mode-3 epilogue of BN2) + weight gradient in one launch; the weight
         gradient's split reduction runs on the side stream.  Returns (gm, partials, blocks per
         segment) like ``_dgrad`` with ``bn_epi=("mask", ...)``."""
         Nb, H, W, Ci = a_prev.shape
         Co = cs.conv.out_channels
         M = Nb * H * W
-        bps = self._dual_bps(M // S)
+        bps = self._bwd1x1_bps(M // S)
         w = shadow_ohwi(cs.conv.weight, Ci)
         wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
         dev = dyn.device
@@ -970,9 +973,9 @@ class FusedStages:
             a_prev, bs_prev = tp.acts[i - 1], tp.bns[i - 1]
             _ext.TAG = f"{b.name} conv{i + 1} dgrad"
             dyn, bnb = (g3, lazy) if (i == L and lazy is not None) else (da, None)
-            if self._dual_ok(cs, dyn, xin, pro_ss, a_prev, S):
+            if self._bwd1x1_ok(cs, dyn, xin, pro_ss, a_prev, S):
                 _ext.TAG = f"{b.name} conv{i + 1} dgrad+wgrad"
-                gm, part, nb = self._dual_backward(ops, dyn, bnb, cs, a_prev, bs_prev, S)
+                gm, part, nb = self._bwd1x1_fused(ops, dyn, bnb, cs, a_prev, bs_prev, S)
                 h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
             else:
                 gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,
