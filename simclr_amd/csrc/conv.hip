@@ -2292,6 +2292,7 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
   uint16_t* Xr = Xs + 2 * BMT * CI;           // [2][64][CI]  raw a2 (epilogue mask / x̂)
   uint16_t* Ws = Xr + 2 * BMT * CI;           // [CI][CO]     Wᵀ, chunk ^= row & 7
   float* red = (float*)(Ws + CI * CO);        // [4][CI][2]   statistics reduction
+  float* Tb = red + 4 * CI * 2;               // [4][CI]      BN2 tables for the epilogue
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -2329,46 +2330,42 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
     xsc[e] = p.xss[seg * CI + ci];
     xsh[e] = p.xss[(p.S + seg) * CI + ci];
   }
-  // epilogue tables of the lane's 16 channels: ci = fn*16 + 4g + r
-  float esc[4][4], esh[4][4], emu[4][4], einv[4][4];
-#pragma unroll
-  for (int fn = 0; fn < 4; ++fn)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ci = fn * 16 + 4 * g + r;
-      esc[fn][r] = p.xss[seg * CI + ci];
-      esh[fn][r] = p.xss[(p.S + seg) * CI + ci];
-      emu[fn][r] = p.xmi[seg * CI + ci];
-      einv[fn][r] = p.xmi[(p.S + seg) * CI + ci];
-    }
+  // epilogue tables (BN2 scale, shift, mean, invstd of this segment) in LDS: [4][CI]
+  for (int i = tid; i < 4 * CI; i += 256) {
+    const int k = i / CI, c = i % CI;
+    Tb[i] = (k < 2 ? p.xss : p.xmi)[((k & 1) * p.S + seg) * CI + c];
+  }
 
-  u32x4 rG[8], rA[8], rX[2];
-  auto gload = [&](int t) {
+  // operand loads run two m-tiles ahead (two register sets, the loop unrolled by two so that
+  // every set index is static): one tile's 72 KB per block is too little in flight to cover
+  // HBM latency at one block per CU
+  u32x4 rG[2][8], rA[2][8], rX[2][2];
+  auto gload = [&](int t, u32x4 (&G8)[8], u32x4 (&A8)[8], u32x4 (&X2)[2]) {
     const int m0 = mbeg + t * BMT;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t off = (uint32_t)(((size_t)(m0 + grow + 8 * j) * CO + gch * 8) * 2);
-      rG[j] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
-      if (lazy) rA[j] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+      G8[j] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
+      if (lazy) A8[j] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      rX[j] = __builtin_amdgcn_raw_buffer_load_b128(
+      X2[j] = __builtin_amdgcn_raw_buffer_load_b128(
           rx, (uint32_t)(((size_t)(m0 + xrow + 32 * j) * CI + xch * 8) * 2), 0, 0);
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const u32x4 (&G8)[8], const u32x4 (&A8)[8], const u32x4 (&X2)[2]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int r = grow + 8 * j;
       *(u32x4*)(Ds + buf * BMT * CO + r * CO + tr_swz<CO>(r, gch * 8)) =
-          lazy ? bnbwd8(rG[j], rA[j], cA, cB, cD, true) : rG[j];
+          lazy ? bnbwd8(G8[j], A8[j], cA, cB, cD, true) : G8[j];
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int r = xrow + 32 * j;
       *(u32x4*)(Xs + buf * BMT * CI + r * CI + tr_swz<CI>(r, xch * 8)) =
-          affine_relu8(rX[j], xsc, xsh, true, true);
-      *(u32x4*)(Xr + buf * BMT * CI + r * CI + xch * 8) = rX[j];
+          affine_relu8(X2[j], xsc, xsh, true, true);
+      *(u32x4*)(Xr + buf * BMT * CI + r * CI + xch * 8) = X2[j];
     }
   };
 
@@ -2383,15 +2380,10 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) { s1[i][j] = 0.f; s2[i][j] = 0.f; }
 
-  if (T > 0) {
-    gload(0);
-    lstore(0);
-  }
-  __syncthreads();
-  typedef short i16x8 __attribute__((ext_vector_type(8)));
-  for (int t = 0; t < T; ++t) {
+  // tile t computes from LDS buffer t & 1; register set (t + 1) & 1 holds tile t + 1 (stored to
+  // LDS at the end of iteration t); the loads of tile t + 2 go into set t & 1 at its start
+  auto compute = [&](int t) {
     const int cur = t & 1;
-    if (t + 1 < T) gload(t + 1);
     const uint16_t* Db = Ds + cur * BMT * CO;
     // dgrad: D[ci][m] over k = co; wave owns rows m = wid*16 + li
     f32x4 accd[4];
@@ -2418,19 +2410,42 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
     for (int fn = 0; fn < 4; ++fn) {
       const int ci = fn * 16 + 4 * g;
       const u32x2 yv = *(const u32x2*)(xr + ci);
+      const float4 tsc = *(const float4*)(Tb + ci), tsh = *(const float4*)(Tb + CI + ci);
+      const float4 tmu = *(const float4*)(Tb + 2 * CI + ci);
+      const float4 tin = *(const float4*)(Tb + 3 * CI + ci);
       const float y[4] = {lo_bf(yv.x), hi_bf(yv.x), lo_bf(yv.y), hi_bf(yv.y)};
+      const float sc4[4] = {tsc.x, tsc.y, tsc.z, tsc.w}, sh4[4] = {tsh.x, tsh.y, tsh.z, tsh.w};
+      const float mu4[4] = {tmu.x, tmu.y, tmu.z, tmu.w}, in4[4] = {tin.x, tin.y, tin.z, tin.w};
       float gv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float a = bf2f(f2bf(accd[fn][r]));
-        gv[r] = y[r] * esc[fn][r] + esh[fn][r] > 0.f ? a : 0.f;
+        gv[r] = y[r] * sc4[r] + sh4[r] > 0.f ? a : 0.f;
         s1[fn][r] += gv[r];
-        s2[fn][r] += gv[r] * ((y[r] - emu[fn][r]) * einv[fn][r]);
+        s2[fn][r] += gv[r] * ((y[r] - mu4[r]) * in4[r]);
       }
       const u32x2 w = {pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
       __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CI + ci));
     }
-    if (t + 1 < T) lstore(cur ^ 1);
+  };
+
+  if (T > 0) {
+    gload(0, rG[0], rA[0], rX[0]);
+    lstore(0, rG[0], rA[0], rX[0]);
+  }
+  if (T > 1) gload(1, rG[1], rA[1], rX[1]);
+  __syncthreads();
+  for (int t = 0; t < T; t += 2) {
+    // even tile t: set 1 holds t + 1, set 0 is free
+    if (t + 2 < T) gload(t + 2, rG[0], rA[0], rX[0]);
+    compute(t);
+    if (t + 1 < T) lstore(1, rG[1], rA[1], rX[1]);
+    __syncthreads();
+    if (t + 1 >= T) break;
+    // odd tile t + 1: set 0 holds t + 2, set 1 is free
+    if (t + 3 < T) gload(t + 3, rG[1], rA[1], rX[1]);
+    compute(t + 1);
+    if (t + 2 < T) lstore(0, rG[0], rA[0], rX[0]);
     __syncthreads();
   }
   // dW slab of this block: [co][ci]
@@ -2761,7 +2776,7 @@ void conv_weight_transform(const uint16_t* W, uint16_t* Wt, int Co, int KH, int 
 
 size_t conv1x1_bwd_dual_lds() {
   return (size_t)2 * 64 * 256 * 2 + 2 * (size_t)2 * 64 * 64 * 2 + (size_t)64 * 256 * 2 +
-         (size_t)4 * 64 * 2 * 4;
+         (size_t)4 * 64 * 2 * 4 + (size_t)4 * 64 * 4;
 }
 
 void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, const uint16_t* X,
