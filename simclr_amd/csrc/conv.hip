@@ -1382,7 +1382,11 @@ __device__ __forceinline__ void wgrad_store(const WgradArgs& p,
     }
 }
 
-template <int BCO, int BKK, int WM, int WN, bool PRO, bool DPRO>
+// DEEP: operand loads run two 64-row steps ahead in two register sets (loop unrolled by two, every
+// set index static).  With one set the loads of step it+1 have only step it's MFMAs (~0.4 µs at
+// two waves per SIMD) to arrive, less than an L2 / MALL round trip under load: the layer3 3x3
+// weight gradient measured MFMA-busy 23 % with 3.6 VALU per MFMA (r3 log).
+template <int BCO, int BKK, int WM, int WN, bool PRO, bool DPRO, bool DEEP = false>
 __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn(WgradArgs p) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
   constexpr int FM = TCO / 16, FN = TKK / 16;
@@ -1426,8 +1430,11 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
   const int kw = tap - kh * p.KW;
   const int OHW = p.OH * p.OW;
 
-  u32x4 rd[DCH], rx[XCH], rd2[DCH];
-  bool dok[DCH];
+  struct Stage {
+    u32x4 rd[DCH], rx[XCH], rd2[DCH];
+    bool dok[DCH], xok[XCH], xseg[XCH];
+  };
+  Stage S0, S1;
   float dA[8], dB[8], dD[8];
   const __amdgpu_buffer_rsrc_t rd2_src = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(DPRO ? p.dY2 : p.dY), (short)0, (int)p.dy_bytes, 0x00020000);
@@ -1441,8 +1448,6 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
       dD[e] = p.dp_coef[(2 * p.dp_S + dseg) * p.N + cc + e];
     }
   }
-  bool xok[XCH];
-  bool xseg[XCH];
   constexpr bool pro = PRO;
   float psc0[8], psh0[8], psc1[8], psh1[8];
   if (pro) {
@@ -1482,16 +1487,16 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
   const uint32_t dstep = (uint32_t)(64 * p.N * 2);
   const int cstride = p.C * 2;
 
-  auto gload = [&](int it) {
+  auto gload = [&](int it, Stage& st) {
     const int mb = mbeg + it * 64;
 #pragma unroll
     for (int j = 0; j < DCH; ++j) {
       const int m = mb + drow + RD * j;
       const bool ok = m < mend && dcol_ok;
-      rd[j] = __builtin_amdgcn_raw_buffer_load_b128(rd_src, ok ? doff[j] : p.dy_bytes, 0, 0);
+      st.rd[j] = __builtin_amdgcn_raw_buffer_load_b128(rd_src, ok ? doff[j] : p.dy_bytes, 0, 0);
       if (DPRO) {
-        rd2[j] = __builtin_amdgcn_raw_buffer_load_b128(rd2_src, ok ? doff[j] : p.dy_bytes, 0, 0);
-        dok[j] = ok;
+        st.rd2[j] = __builtin_amdgcn_raw_buffer_load_b128(rd2_src, ok ? doff[j] : p.dy_bytes, 0, 0);
+        st.dok[j] = ok;
       }
       doff[j] += dstep;
     }
@@ -1504,13 +1509,13 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
       const int iw = (int)__umul24((unsigned)xow[j], (unsigned)p.isw) + iwb;
       const bool ok = m < mend && k_ok && (unsigned)ih < (unsigned)p.IH &&
                       (unsigned)iw < (unsigned)p.IW;
-      xok[j] = ok;
-      xseg[j] = pro && m >= p.pro_seg_rows;
+      st.xok[j] = ok;
+      st.xseg[j] = pro && m >= p.pro_seg_rows;
       const uint32_t pix =
           __umul24(__umul24((unsigned)xn[j], (unsigned)p.IH) + (unsigned)ih, (unsigned)p.IW) +
           (unsigned)iw;
       const uint32_t off = ok ? __umul24(pix, (unsigned)cstride) + (uint32_t)(ci * 2) : p.x_bytes;
-      rx[j] = __builtin_amdgcn_raw_buffer_load_b128(rx_src, off, 0, 0);
+      st.rx[j] = __builtin_amdgcn_raw_buffer_load_b128(rx_src, off, 0, 0);
       // advance this chunk's output pixel by 64 rows
       int ow = xow[j] + dow, oh = xoh[j] + doh, n = xn[j] + dn;
       if (ow >= p.OW) { ow -= p.OW; ++oh; }
@@ -1518,17 +1523,17 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
       xow[j] = ow; xoh[j] = oh; xn[j] = n;
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const Stage& st) {
 #pragma unroll
     for (int j = 0; j < DCH; ++j)
       *(u32x4*)(Ds + buf * 64 * SD + (drow + RD * j) * SD + tr_swz<BCO>(drow + RD * j, dch * 8)) =
-          DPRO ? bnbwd8(rd[j], rd2[j], dA, dB, dD, dok[j]) : rd[j];
+          DPRO ? bnbwd8(st.rd[j], st.rd2[j], dA, dB, dD, st.dok[j]) : st.rd[j];
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
-      u32x4 v = rx[j];
+      u32x4 v = st.rx[j];
       if (pro)
-        v = xseg[j] ? affine_relu8(v, psc1, psh1, xok[j], p.pro_relu != 0)
-                    : affine_relu8(v, psc0, psh0, xok[j], p.pro_relu != 0);
+        v = st.xseg[j] ? affine_relu8(v, psc1, psh1, st.xok[j], p.pro_relu != 0)
+                       : affine_relu8(v, psc0, psh0, st.xok[j], p.pro_relu != 0);
       *(u32x4*)(Xs + buf * 64 * SX + (xrow + RX * j) * SX + tr_swz<BKK>(xrow + RX * j, xch * 8)) = v;
     }
   };
@@ -1540,16 +1545,34 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   if (nit > 0) {
-    gload(0);
-    lstore(0);
+    gload(0, S0);
+    lstore(0, S0);
   }
-  __syncthreads();
-  for (int it = 0; it < nit; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < nit) gload(it + 1);
-    wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * SD, Xs + cur * 64 * SX, acc);
-    if (it + 1 < nit) lstore(cur ^ 1);
+  if constexpr (!DEEP) {
     __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < nit) gload(it + 1, S0);
+      wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * SD, Xs + cur * 64 * SX, acc);
+      if (it + 1 < nit) lstore(cur ^ 1, S0);
+      __syncthreads();
+    }
+  } else {
+    // entering an even step it: LDS buffer 0 holds step it, S1 step it + 1, S0 step it + 2
+    if (nit > 1) gload(1, S1);
+    if (nit > 2) gload(2, S0);
+    __syncthreads();
+    for (int it = 0; it < nit; it += 2) {
+      wgrad_mma<BCO, BKK, WM, WN>(Ds, Xs, acc);
+      if (it + 1 < nit) lstore(1, S1);
+      __syncthreads();
+      if (it + 3 < nit) gload(it + 3, S1);
+      if (it + 1 >= nit) break;
+      wgrad_mma<BCO, BKK, WM, WN>(Ds + 64 * SD, Xs + 64 * SX, acc);
+      if (it + 2 < nit) lstore(0, S0);
+      __syncthreads();
+      if (it + 4 < nit) gload(it + 4, S0);
+    }
   }
   wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
   const int kb[1] = {k0};
@@ -2187,7 +2210,7 @@ void launch_igemm(const IgemmArgs& a, hipStream_t s) {
   }
 }
 
-template <int BCO, int BKK, int WM, int WN>
+template <int BCO, int BKK, int WM, int WN, bool DEEP = false>
 void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   const bool pro = a0.pro_sc != nullptr;
   const bool dpro = a0.dY2 != nullptr;
@@ -2197,13 +2220,13 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   const int grid = a.nCo * a.nKk * a.splits;
   const size_t lds = (size_t)2 * 64 * (BCO + BKK) * 2;
   if (pro && dpro)
-    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true, true>), dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true, true, DEEP>), dim3(grid), dim3(256), lds, s, a);
   else if (pro)
-    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true, false>), dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, true, false, DEEP>), dim3(grid), dim3(256), lds, s, a);
   else if (dpro)
-    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false, true>), dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false, true, DEEP>), dim3(grid), dim3(256), lds, s, a);
   else
-    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false, false>), dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((wgrad_tn<BCO, BKK, WM, WN, false, false, DEEP>), dim3(grid), dim3(256), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -2248,9 +2271,14 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {256, 128, 256}, {128, 256, 256}, {256, 256, 256},
                                   {64, 256, 512},  {128, 128, 256}, {64, 256, 256},
                                   {128, 64, 512},  {128, 128, 256}, {64, 128, 512},
-                                  {256, 128, 256}, {64, 64, 256}};
+                                  {256, 128, 256}, {64, 64, 256},
+                                  {64, 128, 768}, {128, 64, 768}};
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
+// wgrad_tn with loads two steps ahead (DEEP): the 64 x 128 / 128 x 64 tiles gain 10-17 % on the
+// 3x3 / 1x1 weight gradients (tools/wgrad_probe.py); the 128 x 128 and 256 x 64 DEEP tiles spill
+// at the 256-VGPR cap of two blocks per CU and lose (not instantiated)
+constexpr int WG_DEEP0 = 18;
 
 
 // -------------------------------------------------- fused 1x1 backward: dgrad + wgrad in one pass
@@ -2614,10 +2642,11 @@ int igemm_tail_ticket_words(int nNb, int S, int ngrp) { return nNb * S * ngrp + 
 
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
-bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < wgrad_num_variants(); }
+bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < WG_PATCH0; }
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
-  if (v >= WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
+  if (v == WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
+  if (v >= WG_DEEP0) return true;  // register-staged: every prologue
   // wgrad_glds has the X-operand BN-apply prologue only (no dY BN-backward prologue)
   return v < WG_GLDS0 || (!dy_pro && igemm_glds_ok(g, pro, false));
 }
@@ -2627,7 +2656,7 @@ int wgrad_splits(const ConvGeom& g, int variant) {
   const int bco = WG_VARIANTS[variant][0], bkk = WG_VARIANTS[variant][1];
   const int M = g.Nb * g.OH * g.OW;
   const int K = g.KH * g.KW * g.C;
-  const bool patch = variant >= WG_PATCH0;
+  const bool patch = variant == WG_PATCH0;
   // the patch kernel's K tile is all 9 taps of 64 input channels; its M unit is 256 rows
   const int tiles = ((g.N + bco - 1) / bco) * (patch ? g.C / 64 : (K + bkk - 1) / bkk);
   const int iters = patch ? M / 256 : (M + 63) / 64;
@@ -2661,7 +2690,7 @@ int wgrad_splits(const ConvGeom& g, int variant) {
 int wgrad_tiles(const ConvGeom& g, int variant) {
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
   const int K = g.KH * g.KW * g.C;
-  if (variant >= WG_PATCH0) return (g.N / 64) * (g.C / 64);
+  if (variant == WG_PATCH0) return (g.N / 64) * (g.C / 64);
   const int bco = WG_VARIANTS[variant][0], bkk = WG_VARIANTS[variant][1];
   return ((g.N + bco - 1) / bco) * ((K + bkk - 1) / bkk);
 }
@@ -2681,7 +2710,7 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.ish = g.ish; a.isw = g.isw; a.dh = g.dh; a.dw = g.dw; a.ih0 = g.ih0; a.iw0 = g.iw0;
   a.dy_bytes = (uint32_t)((size_t)a.M * a.N * 2);
   a.x_bytes = (uint32_t)(x_elems * 2);
-  const int iters = variant >= WG_PATCH0 ? a.M / 256 : (a.M + 63) / 64;
+  const int iters = variant == WG_PATCH0 ? a.M / 256 : (a.M + 63) / 64;
   a.splits = splits;
   a.iters_per_split = (iters + splits - 1) / splits;
   a.pro_sc = f.pro_sc; a.pro_sh = f.pro_sh;
@@ -2727,6 +2756,8 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
       HIP_CHECK_LAUNCH();
       break;
     }
+    case 18: launch_wgrad<64, 128, 2, 2, true>(a, s); break;
+    case 19: launch_wgrad<128, 64, 2, 2, true>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;
