@@ -847,6 +847,32 @@ void check_nt(int R, int Ccols, int D, int col_offset, int n_local) {
   TORCH_CHECK(col_offset >= 0 && col_offset + R <= Ccols, "ntxent: bad col_offset");
 }
 int64_t nt_fwd_splits(int64_t R, int64_t C) { return ntxent_fwd_splits(R, C); }
+// rows [R][D] -> columns [c0, c0 + R) of out [D][Ccols]
+void nt_transpose_cols(const Tensor& in, const Tensor& out, int64_t c0) {
+  const int R = in.size(0), D = in.size(1);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == D && c0 >= 0 && c0 + R <= out.size(1),
+              "nt_transpose_cols: out must be [D][Ccols] with room for columns [c0, c0 + R)");
+  ntxent_transpose_cols(f32(in, "in"), f32w(out, "out"), R, D, (int)out.size(1), (int)c0,
+                        cur_stream());
+}
+// forward partials of columns [c_lo, c_hi) into splits [split_base, split_base + splits)
+void nt_forward_range(const Tensor& znT, int64_t R, int64_t col_offset, int64_t n_local,
+                      double inv_temp, const Tensor& part, int64_t c_lo, int64_t c_hi,
+                      int64_t splits, int64_t split_base) {
+  const int D = znT.size(0), Ccols = znT.size(1);
+  check_nt(R, Ccols, D, col_offset, n_local);
+  TORCH_CHECK(c_lo >= 0 && c_lo < c_hi && c_hi <= Ccols && c_lo % 16 == 0 && c_hi % 16 == 0 &&
+                  splits >= 1 && split_base >= 0 && part.numel() >= (split_base + splits) * R * 3,
+              "nt_forward_range: column window / splits");
+  ntxent_forward_range(f32(znT, "znT"), R, Ccols, D, col_offset, n_local, (float)inv_temp,
+                       f32w(part, "part"), c_lo, c_hi, splits, split_base, cur_stream());
+}
+void nt_finish(const Tensor& part, int64_t R, int64_t splits, const Tensor& lse,
+               const Tensor& loss) {
+  TORCH_CHECK(part.numel() >= splits * R * 3 && lse.numel() == R && loss.numel() == R,
+              "nt_finish sizes");
+  ntxent_finish(f32(part, "part"), R, splits, f32w(lse, "lse"), f32w(loss, "loss"), cur_stream());
+}
 int64_t nt_bwd_splits(int64_t nown, int64_t npart) { return ntxent_bwd_splits(nown, npart); }
 void nt_forward(const Tensor& znT, int64_t R, int64_t col_offset, int64_t n_local, double inv_temp,
                 const Tensor& part, int64_t splits, const Tensor& lse, const Tensor& loss) {
@@ -1049,6 +1075,9 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("cast_to_f32(Tensor x, Tensor(a!) y) -> ()", &cast_to_f32);
   m.def("nt_normalize(Tensor z, Tensor(a!) zn, Tensor(b!) inv_norm) -> ()", &nt_normalize);
   m.def("nt_transpose(Tensor x, Tensor(a!) out) -> ()", &nt_transpose);
+  m.def("nt_transpose_cols(Tensor x, Tensor(a!) out, int c0) -> ()", &nt_transpose_cols);
+  m.def("nt_forward_range(Tensor znT, int R, int col_offset, int n_local, float inv_temp, Tensor(a!) part, int c_lo, int c_hi, int splits, int split_base) -> ()", &nt_forward_range);
+  m.def("nt_finish(Tensor part, int R, int splits, Tensor(a!) lse, Tensor(b!) loss) -> ()", &nt_finish);
   m.def("nt_fwd_splits(int R, int C) -> int", &nt_fwd_splits);
   m.def("nt_bwd_splits(int nown, int npart) -> int", &nt_bwd_splits);
   m.def("nt_forward(Tensor znT, int R, int col_offset, int n_local, float inv_temp, Tensor(a!) part, int splits, Tensor(b!) lse, Tensor(c!) loss) -> ()", &nt_forward);

@@ -218,6 +218,14 @@ void cast_bf16_f32(const uint16_t* x, float* y, size_t n, hipStream_t s);
 void ntxent_normalize_f32(const uint16_t* z, int R, int D, float* zn, float* inv_norm,
                           hipStream_t s);
 void ntxent_transpose(const float* in, float* out, int R, int D, hipStream_t s);
+// in [R][D] -> columns [c0, c0 + R) of out [D][ldo]
+void ntxent_transpose_cols(const float* in, float* out, int R, int D, int ldo, int c0,
+                           hipStream_t s);
+// forward partials of the columns [c_lo, c_hi) into splits [split_base, +splits), and the merge
+void ntxent_forward_range(const float* znT, int R, int Ccols, int D, int col_offset, int n_local,
+                          float inv_temp, float* part, int c_lo, int c_hi, int splits,
+                          int split_base, hipStream_t s);
+void ntxent_finish(const float* part, int R, int splits, float* lse, float* loss, hipStream_t s);
 int ntxent_fwd_splits(int R, int Ccols);
 int ntxent_bwd_splits(int nown, int npart);
 void ntxent_forward(const float* znT, int R, int Ccols, int D, int col_offset, int n_local,

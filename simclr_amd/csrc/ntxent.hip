@@ -47,8 +47,9 @@ __global__ void k_normalize(const uint16_t* __restrict__ z, int R, int D, float*
   if (lane == 0) inv_norm[row] = inv;
 }
 
-// in [R][D] -> out [D][R]
-__global__ void k_transpose(const float* __restrict__ in, float* __restrict__ out, int R, int D) {
+// in [R][D] -> out [D][ldo] at columns [c0, c0 + R)
+__global__ void k_transpose(const float* __restrict__ in, float* __restrict__ out, int R, int D,
+                            int ldo, int c0) {
   __shared__ float t[32][33];
   const int r0 = blockIdx.x * 32, d0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: ty 0..7
@@ -59,7 +60,7 @@ __global__ void k_transpose(const float* __restrict__ in, float* __restrict__ ou
   __syncthreads();
   for (int k = ty; k < 32; k += 8) {
     const int d = d0 + k, r = r0 + tx;
-    if (d < D && r < R) out[(size_t)d * R + r] = t[tx][k];
+    if (d < D && r < R) out[(size_t)d * ldo + c0 + r] = t[tx][k];
   }
 }
 
@@ -87,14 +88,15 @@ template <int D>
 __global__ __launch_bounds__(64) void k_ntxent_fwd(const float* __restrict__ znT, int R, int Ccols,
                                                    int col_offset, int n_local,
                                                    float inv_temp, int cols_per_split,
-                                                   float* __restrict__ part) {
+                                                   float* __restrict__ part, int c_lo, int c_hi,
+                                                   int split_base) {
   const int lane = threadIdx.x;
   const int g = lane >> 4, li = lane & 15;
   const int r0 = blockIdx.x * 16;
-  const int split = blockIdx.y;
-  const int c_beg = split * cols_per_split;
+  const int split = split_base + blockIdx.y;
+  const int c_beg = c_lo + blockIdx.y * cols_per_split;
   int c_end = c_beg + cols_per_split;
-  if (c_end > Ccols) c_end = Ccols;
+  if (c_end > c_hi) c_end = c_hi;
   float breg[D / 4];
 #pragma unroll
   for (int ks = 0; ks < D / 4; ++ks)
@@ -315,10 +317,15 @@ void ntxent_normalize_f32(const uint16_t* z, int R, int D, float* zn, float* inv
   HIP_CHECK_LAUNCH();
 }
 
-void ntxent_transpose(const float* in, float* out, int R, int D, hipStream_t s) {
+void ntxent_transpose_cols(const float* in, float* out, int R, int D, int ldo, int c0,
+                           hipStream_t s) {
   hipLaunchKernelGGL(k_transpose, dim3((R + 31) / 32, (D + 31) / 32), dim3(256), 0, s, in, out, R,
-                     D);
+                     D, ldo, c0);
   HIP_CHECK_LAUNCH();
+}
+
+void ntxent_transpose(const float* in, float* out, int R, int D, hipStream_t s) {
+  ntxent_transpose_cols(in, out, R, D, R, 0, s);
 }
 
 // measured optimum (tools/ntxent_bench.py, 8192 columns): ~16 partner tiles per block for the
@@ -328,15 +335,16 @@ int ntxent_bwd_splits(int nown, int npart) {
   return splits_for(nown / 16, npart / 16, nown <= npart ? 8 : 16);
 }
 
-void ntxent_forward(const float* znT, int R, int Ccols, int D, int col_offset, int n_local,
-                    float inv_temp, float* part, int splits, float* lse, float* loss,
-                    hipStream_t s) {
-  const int ptiles = Ccols / 16;
+// columns [c_lo, c_hi) of znT into splits [split_base, split_base + splits) of part
+void ntxent_forward_range(const float* znT, int R, int Ccols, int D, int col_offset, int n_local,
+                          float inv_temp, float* part, int c_lo, int c_hi, int splits,
+                          int split_base, hipStream_t s) {
+  const int ptiles = (c_hi - c_lo) / 16;
   const int per = ((ptiles + splits - 1) / splits) * 16;
 #define FWD_CASE(DD)                                                                        \
   case DD:                                                                                  \
     hipLaunchKernelGGL(k_ntxent_fwd<DD>, dim3(R / 16, splits), dim3(64), 0, s, znT, R, Ccols, \
-                       col_offset, n_local, inv_temp, per, part);                           \
+                       col_offset, n_local, inv_temp, per, part, c_lo, c_hi, split_base);   \
     break;
   switch (D) {
     FWD_CASE(32) FWD_CASE(64) FWD_CASE(128) FWD_CASE(256)
@@ -344,9 +352,20 @@ void ntxent_forward(const float* znT, int R, int Ccols, int D, int col_offset, i
   }
 #undef FWD_CASE
   HIP_CHECK_LAUNCH();
+}
+
+void ntxent_finish(const float* part, int R, int splits, float* lse, float* loss, hipStream_t s) {
   hipLaunchKernelGGL(k_ntxent_finish, dim3((R + 255) / 256), dim3(256), 0, s, part, R, splits, lse,
                      loss);
   HIP_CHECK_LAUNCH();
+}
+
+void ntxent_forward(const float* znT, int R, int Ccols, int D, int col_offset, int n_local,
+                    float inv_temp, float* part, int splits, float* lse, float* loss,
+                    hipStream_t s) {
+  ntxent_forward_range(znT, R, Ccols, D, col_offset, n_local, inv_temp, part, 0, Ccols, splits, 0,
+                       s);
+  ntxent_finish(part, R, splits, lse, loss, s);
 }
 
 void ntxent_backward_part(int row_mode, const float* zn, const float* znT, const float* lse, int R,

@@ -7,10 +7,11 @@ target is the same image's other view; ``reduction="mean"`` averages over the 2N
 ``"sum"`` sums, ``"none"`` returns a (2, N) tensor [view0 anchors; view1 anchors].
 
 Extension (north star): ``gather=True`` all-gathers the bf16 embeddings z of every
-rank over RCCL (each rank then normalises all of them), so each anchor sees 2·N·W − 1
-candidates instead of 2N − 1 (negatives from the global batch).  The gradient w.r.t. the
-gathered columns returns through a reduce-scatter on a side stream, overlapped with the
-row-gradient kernel.
+rank over RCCL on a side stream, overlapped with this rank's normalisation and the scoring of
+its own columns (the peers' columns are scored into further online-LSE partials once they
+arrive), so each anchor sees 2·N·W − 1 candidates instead of 2N − 1 (negatives from the global
+batch).  The gradient w.r.t. the gathered columns returns through a reduce-scatter on a side
+stream, overlapped with the row-gradient kernel.
 Parity default is ``gather=False`` (the reference's loss is per-GPU local).
 
 GPU path: the fused exact-fp32 MFMA kernels of ``csrc/ntxent.hip`` (no N×N logits, no mask or
@@ -73,36 +74,62 @@ class _NTXentHipFn(torch.autograd.Function):
         R, D = z.shape
         dev = z.device
         zb = z.contiguous() if z.dtype == torch.bfloat16 else z.to(torch.bfloat16).contiguous()
+        inv_t = 1.0 / temperature
+        lse = torch.empty((R,), device=dev, dtype=torch.float32)
+        rows = torch.empty((R,), device=dev, dtype=torch.float32)
         if gather and st.comm:
-            # global negatives: the ranks exchange bf16 z (half the bytes of gathering fp32 ẑ)
-            # and every rank normalises all W·R rows with the same row-wise kernel, so its copy
-            # of a peer's ẑ is bitwise the peer's own.  The exchange sits between the head and the
-            # loss (nothing else in the step is independent of it); at 8 ranks it moves 8 x 256
-            # KiB, latency-bound on RCCL's launch floor
+            # global negatives: the ranks exchange bf16 z (half the bytes of gathering fp32 ẑ) on
+            # a side stream.  Meanwhile this rank normalises its own rows and scores them against
+            # its OWN columns (their online log-sum-exp partials, the positive included); after
+            # the exchange every rank normalises the peers' rows with the same row-wise kernel
+            # (its copy of a peer's ẑ is bitwise the peer's own) and scores the remaining
+            # columns into further split partials; one merge gives lse and the loss.
             W = st.world_size
             col_offset = st.rank * R
-            zb_all = torch.empty((W * R, D), device=dev, dtype=torch.bfloat16)
-            dist.all_gather_into_tensor(zb_all, zb, group=st.group)
-            zall = torch.empty((W * R, D), device=dev, dtype=torch.float32)
-            inv_all = torch.empty((W * R,), device=dev, dtype=torch.float32)
-            ops.nt_normalize(zb_all, zall, inv_all)
+            Ccols = W * R
+            cur = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(cur)
+            zb_all = torch.empty((Ccols, D), device=dev, dtype=torch.bfloat16)
+            with torch.cuda.stream(side):
+                dist.all_gather_into_tensor(zb_all, zb, group=st.group)
+            zall = torch.empty((Ccols, D), device=dev, dtype=torch.float32)
+            inv_all = torch.empty((Ccols,), device=dev, dtype=torch.float32)
             zn = zall[col_offset:col_offset + R]
             inv = inv_all[col_offset:col_offset + R]
+            znT = torch.empty((D, Ccols), device=dev, dtype=torch.float32)
+            ops.nt_normalize(zb, zn, inv)
+            ops.nt_transpose_cols(zn, znT, col_offset)
+            s_loc = ops.nt_fwd_splits(R, R)
+            s_rem = ops.nt_fwd_splits(R, Ccols - R)
+            part = torch.empty(((s_loc + 2 * s_rem) * R * 3,), device=dev, dtype=torch.float32)
+            ops.nt_forward_range(znT, R, col_offset, n, inv_t, part, col_offset, col_offset + R,
+                                 s_loc, 0)  # overlaps the exchange
+            cur.wait_stream(side)
+            zb_all.record_stream(cur)
+            # every row in one launch each (this rank's block is rewritten with identical
+            # values, after the local scoring read it: same stream)
+            ops.nt_normalize(zb_all, zall, inv_all)
+            ops.nt_transpose(zall, znT)
+            nsp = s_loc
+            for lo, hi in ((0, col_offset), (col_offset + R, Ccols)):
+                if hi > lo:
+                    sp = max(1, (s_rem * (hi - lo) + (Ccols - R) - 1) // (Ccols - R))
+                    ops.nt_forward_range(znT, R, col_offset, n, inv_t, part, lo, hi, sp, nsp)
+                    nsp += sp
+            ops.nt_finish(part, R, nsp, lse, rows)
         else:
             zn = torch.empty((R, D), device=dev, dtype=torch.float32)
             inv = torch.empty((R,), device=dev, dtype=torch.float32)
             ops.nt_normalize(zb, zn, inv)
             zall = zn
             col_offset = 0
-        Ccols = zall.shape[0]
-        znT = torch.empty((D, Ccols), device=dev, dtype=torch.float32)
-        ops.nt_transpose(zall, znT)
-        splits = ops.nt_fwd_splits(R, Ccols)
-        part = torch.empty((splits * R * 3,), device=dev, dtype=torch.float32)
-        lse = torch.empty((R,), device=dev, dtype=torch.float32)
-        rows = torch.empty((R,), device=dev, dtype=torch.float32)
-        inv_t = 1.0 / temperature
-        ops.nt_forward(znT, R, col_offset, n, inv_t, part, splits, lse, rows)
+            Ccols = R
+            znT = torch.empty((D, Ccols), device=dev, dtype=torch.float32)
+            ops.nt_transpose(zall, znT)
+            splits = ops.nt_fwd_splits(R, Ccols)
+            part = torch.empty((splits * R * 3,), device=dev, dtype=torch.float32)
+            ops.nt_forward(znT, R, col_offset, n, inv_t, part, splits, lse, rows)
         out = torch.empty((1,), device=dev, dtype=torch.float32)
         scale = 1.0 / R if reduction == "mean" else 1.0
         ops.nt_reduce_loss(rows, scale, out)
