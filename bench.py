@@ -157,6 +157,22 @@ def run_ours(args, rank, world, dev):
 
     auto = args.graph == "auto"
     t_eager = None
+    if tr.hip and st.ipc is not None and os.environ.get("SIMCLR_BN_COMM", "auto") == "auto":
+        # statistics-exchange autotune (N > 1): the IPC arena exchange (one-shot stores over
+        # xGMI, spin on LL words) vs the RCCL all-reduce, 3 eager steps each after a warm-up,
+        # the slower of the ranks decides (same choice everywhere)
+        timed(2)
+        if not ipc_guard():
+            t_ipc = timed(3)
+            ex, st.ipc = st.ipc, None
+            t_rccl = timed(3)
+            tt = torch.tensor([t_ipc, t_rccl, float(ex.failed())], dtype=torch.float64,
+                              device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            if float(tt[0]) < float(tt[1]) and float(tt[2]) == 0.0:
+                st.ipc = ex
+            args.comm_probe_ms = [round(float(v) / 3 * 1000.0, 3) for v in tt.tolist()[:2]]
+            args.bn_comm = "ipc" if st.ipc is not None else "rccl(probe)"
     if auto and tr.hip:
         timed(2)  # eager warm-up: autotuning, allocator, communicators
         if ipc_guard():
@@ -372,6 +388,7 @@ def main(argv=None):
             "hip_graph": bool(args.graph and args.impl == "ours"),
             "exec_mode_probe_ms_eager_graph": getattr(args, "mode_probe_ms", None),
             "bn_stats_comm": args.bn_comm,
+            "bn_comm_probe_ms_ipc_rccl": getattr(args, "comm_probe_ms", None),
             "host_issue_ms_per_step": (round(args.host_issue_ms, 3)
                                        if hasattr(args, "host_issue_ms") else None),
             "final_loss": loss,
