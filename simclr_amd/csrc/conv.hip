@@ -28,6 +28,8 @@
 #include "kernels.h"
 #include "bn_tail.h"
 
+#include <type_traits>
+
 namespace {
 
 struct IgemmArgs {
@@ -1099,8 +1101,23 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
 
-  // ---- patch DMA: one wave-instruction = 1 KiB = 64 lanes x 16 B (8 or 16 chunks per pixel)
   const int CPP = C / 8;
+  // PRO: chunk c = tid + i·NT of the landed patch sits in pixel q = tid/CPP + i·(NT/CPP) at
+  // physical chunk tid % CPP (NT % CPP == 0); NT/CPP is a multiple of 8, so q & 7 — and with it
+  // the logical channel chunk (pch ^ (q & 7)) — is the same for every i: the thread's 8 scale /
+  // shift pairs are loaded once, before the DMA (a global load consumed after it would drain
+  // it), and the pixel walk is incremental (no per-chunk division by the patch width)
+  f32x2 psc2[4], psh2[4];
+  if (PRO) {
+    const int pseg = m0 / p.pro_seg_rows;  // block-uniform (host guarantees)
+    const int ch = ((tid % CPP) ^ ((tid / CPP) & 7)) * 8;
+    const float4* ps = (const float4*)(p.pro_sc + pseg * C + ch);
+    const float4* ph = (const float4*)(p.pro_sh + pseg * C + ch);
+    const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+    psc2[0] = {s0.x, s0.y}; psc2[1] = {s0.z, s0.w}; psc2[2] = {s1.x, s1.y}; psc2[3] = {s1.z, s1.w};
+    psh2[0] = {h0.x, h0.y}; psh2[1] = {h0.z, h0.w}; psh2[2] = {h1.x, h1.y}; psh2[3] = {h1.z, h1.w};
+  }
+  // ---- patch DMA: one wave-instruction = 1 KiB = 64 lanes x 16 B (8 or 16 chunks per pixel)
   for (int i = wid; i < ninstr; i += NW) {
     const int q = i * ppi + lane / CPP;  // patch pixel
     const int pch = lane % CPP;
@@ -1151,23 +1168,31 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
     __builtin_amdgcn_s_barrier();
     if (PRO && kt == 0) {
       // the previous BatchNorm's normalise + ReLU, once per patch pixel on the landed patch
-      // (no DMA in flight here); the zero padding of out-of-image pixels stays exactly zero
-      const int pseg = m0 / p.pro_seg_rows;  // block-uniform (host guarantees)
-      const float* psc = p.pro_sc + pseg * C;
-      const float* psh = p.pro_sh + pseg * C;
-      for (int c = tid; c < PP * CPP; c += NT) {
-        const int q = c / CPP, pch = c - q * CPP;
-        const int pr = q / PW, pc = q - pr * PW;
-        const int ih = row0 - 1 + pr, iw = pc - 1;
-        if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
-          const int ch = (pch ^ (q & 7)) * 8;
-          const float4 s0 = *(const float4*)(psc + ch), s1 = *(const float4*)(psc + ch + 4);
-          const float4 h0 = *(const float4*)(psh + ch), h1 = *(const float4*)(psh + ch + 4);
-          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-          u32x4* ptr = (u32x4*)(Ps + q * C + pch * 8);
-          *ptr = affine_relu8(*ptr, sc, sh, true, p.pro_relu != 0);
+      // (no DMA in flight here); the zero padding of out-of-image pixels stays exactly zero.
+      // Four chunks per batch: their LDS reads are all issued before the first write-back.
+      const int QS = NT / CPP;                    // pixel stride of the thread's chunks
+      const int dr = QS / PW, dc = QS - dr * PW;  // ... as (patch rows, patch columns)
+      const int q0 = tid / CPP;
+      int pr = q0 / PW, pc = q0 - pr * PW;
+      uint16_t* base = Ps + tid * 8;              // chunk i at base + i·NT·8
+      const bool relu = p.pro_relu != 0;
+      for (int i0 = 0; i0 * QS + q0 < PP; i0 += 4) {
+        u32x4 v[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ih = row0 - 1 + pr, iw = pc - 1;
+          ok[u] = (i0 + u) * QS + q0 < PP && (unsigned)ih < (unsigned)p.IH &&
+                  (unsigned)iw < (unsigned)p.IW;
+          if (ok[u]) v[u] = *(const u32x4*)(base + (size_t)(i0 + u) * NT * 8);
+          pr += dr;
+          pc += dc;
+          if (pc >= PW) { pc -= PW; ++pr; }
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (ok[u])
+            *(u32x4*)(base + (size_t)(i0 + u) * NT * 8) = affine_relu8_pk(v[u], psc2, psh2, relu);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1203,6 +1228,198 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
   __syncthreads();  // the epilogue reuses the LDS
   igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, smem, m0, n0, mb,
                                           epi_prefetch<EPI>() ? &pre : nullptr);
+}
+
+// ------------------------------------------- 3x3 conv, persistent, resident weights (layer1)
+// The ResNet-50 layer1 3x3 conv (and its stride-1 dgrad): C = N = 64 at 32x32, K = 576.  The
+// per-tile kernel above runs at ~30 % MFMA utilisation: every block waits for its own patch
+// DMA, then for one weight tile per k-step (9 barriers), and only 2 blocks fit a CU.  Here ONE
+// block per CU (8 waves) keeps the whole weight matrix resident in LDS (9 x [64][64], 72 KiB,
+// loaded once) and walks a contiguous run of 256-pixel tiles with a double-buffered input patch:
+// tile t+1's patch is DMA'd while tile t computes, so a tile is 9 taps of MFMAs with no global
+// load or barrier inside them.  Consecutive tiles of a run are the next 8 rows of the same image
+// (their 2 halo rows were just fetched into the XCD's L2).  The epilogue (any mode) stages
+// through the tile's own patch buffer once its MFMAs are done.
+// LDS: weights 73,728 B + 2 patches x 44,032 B + the PRO table 1,024 B = 162,816 B.
+// Host guarantees (igemm_ppatch_ok): igemm_patch_ok geometry with C = N = 64, OW = 32.
+constexpr int PP_NINSTR = 43;                  // patch DMA instructions (8 pixels x 128 B each)
+constexpr int PP_PSZ = PP_NINSTR * 512;        // patch buffer, elements
+constexpr int PP_LDS = 9 * 64 * 64 * 2 + 2 * PP_PSZ * 2 + 1024;
+
+template <int EPI, int PRO>
+__global__ __launch_bounds__(512, 1) void igemm_ppatch(IgemmArgs p) {
+  constexpr int BM = 256, BN = 64, WM = 8, WN = 1, NW = 8, NT = 512;
+  constexpr int TM = BM / WM, FM = TM / 16, FN = BN / 16;  // 2 x 4 fragments per wave
+  constexpr int C = 64, OW = 32, PW = 34, PP = 340, NK = 9;
+  constexpr uint32_t PBYTES = PP_PSZ * 2;  // one patch buffer (44,032 B)
+  constexpr uint32_t WOFF = 2 * PBYTES;    // weights behind the two patches
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Pb = (uint16_t*)smem;                // [2][PP_PSZ] patch images
+  uint16_t* Ws = (uint16_t*)(smem + WOFF);       // [9][64 rows][64], chunk-swizzled (igemm_patch Bs)
+  float* Tb = (float*)(smem + WOFF + NK * BN * 64 * 2);  // PRO: [segment 0, 1][sc, sh][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = p.M / BM;
+  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int t_beg = lbid * per;
+  const int t_end = min(ntiles, t_beg + per);
+  if (t_beg >= t_end) return;  // block-uniform: no barrier is skipped by part of a block
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+
+  if (PRO) {  // both segments' tables, before any DMA (a global load consumed later would drain it)
+    for (int i = tid; i < 2 * 2 * C; i += NT) {
+      const int sg = i / (2 * C), k = (i / C) & 1, c = i % C;
+      const int sgc = sg * p.pro_seg_rows < p.M ? sg : 0;
+      Tb[i] = (k ? p.pro_sh : p.pro_sc)[sgc * C + c];
+    }
+  }
+  // resident weights: k-step kt = rows (co) x 64 (tap kt's channels); lane → (row, chunk)
+  {
+    const int lrow = lane >> 3, lbch = (lane & 7) ^ (lane >> 3);
+    const uint32_t off = (uint32_t)((wid * 8 + lrow) * p.K + lbch * 8) * 2u;
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt)
+      dma16_opaque(rb, Ws + kt * BN * 64 + wid * 8 * 64, off + (uint32_t)(kt * 64) * 2u);
+  }
+  auto issue_patch = [&](int t, uint16_t* P) {
+    const int m0 = t * BM;
+    const int img = m0 / (p.OH * OW);
+    const int row0 = (m0 - img * p.OH * OW) / OW;
+    for (int i = wid; i < PP_NINSTR; i += NW) {
+      const int q = i * 8 + (lane >> 3);
+      const int pch = lane & 7;
+      const int lch = pch ^ (q & 7);
+      const int pr = q / PW, pc = q - (q / PW) * PW;
+      const int ih = row0 - 1 + pr, iw = pc - 1;
+      const bool ok = q < PP && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      const uint32_t off =
+          ok ? (uint32_t)((((img * p.IH + ih) * p.IW + iw) * C + lch * 8) * 2) : p.a_bytes;
+      dma16_opaque(ra, P + i * 512, off);
+    }
+  };
+  issue_patch(t_beg, Pb);
+
+  // Fragment addresses, fixed for every tile: the A fragment of (tap, k-half, fm) is pixel
+  // q = (frow + kh)·PW + fcol + kw at XOR-swizzled chunk (ks·4 + lane/16) ^ (q & 7) — the swizzle
+  // keys on the shifted pixel, so the addresses are not affine in the tap: all 36 are computed
+  // once (VGPR byte offsets into patch buffer 0; buffer 1 is a +44,032 immediate, the tile loop
+  // being unrolled by 2) instead of ~30 VALU of index math per k-half per tile.  The B fragments
+  // of every tap share one row/chunk pattern (the tap is a +8 KiB immediate).
+  uint32_t aoff[NK][2][FM];
+  uint32_t boff[2][FN];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int m = wid * TM + fm * 16 + (lane & 15);
+    const int qb = (m / OW) * PW + (m % OW);
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int q = qb + (kt / 3) * PW + (kt % 3);
+        const int ch = (ks * 4 + (lane >> 4)) ^ (q & 7);
+        aoff[kt][ks][fm] = (uint32_t)(q * C + ch * 8) * 2u;
+      }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int row = fn * 16 + (lane & 15);
+      const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
+      boff[ks][fn] = WOFF + (uint32_t)(row * 64 + ch * 8) * 2u;
+    }
+
+  auto tile = [&](int t, auto curc) {
+    constexpr int cur = decltype(curc)::value;
+    const char* P = smem + cur * PBYTES;
+    const int m0 = t * BM;
+    // this tile's patch (issued a tile ago; the weights too on the first tile) has landed; the
+    // previous tile's 4 output stores per thread, issued after it, may stay in flight
+    if (t == t_beg)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // patch visible to every wave; the other buffer is free
+    if (t + 1 < t_end) issue_patch(t + 1, Pb + (cur ^ 1) * PP_PSZ);
+    if (PRO) {
+      // BN-apply + ReLU on the landed patch (see igemm_patch): chunks 64 pixels apart share
+      // their logical channel chunk; out-of-image pixels stay zero
+      const int pseg = m0 / p.pro_seg_rows;
+      const int img = m0 / (p.OH * OW);
+      const int row0 = (m0 - img * p.OH * OW) / OW;
+      const int q0 = tid >> 3;
+      const int ch = ((tid & 7) ^ (q0 & 7)) * 8;
+      const float4* ps = (const float4*)(Tb + pseg * 2 * C + ch);
+      const float4* ph = (const float4*)(Tb + pseg * 2 * C + C + ch);
+      const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+      const f32x2 sc[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
+      const f32x2 sh[4] = {{h0.x, h0.y}, {h0.z, h0.w}, {h1.x, h1.y}, {h1.z, h1.w}};
+      constexpr int DR = 64 / PW, DC = 64 - DR * PW;
+      int pr = q0 / PW, pc = q0 - (q0 / PW) * PW;
+      uint16_t* base = (uint16_t*)P + tid * 8;
+      const bool relu = p.pro_relu != 0;
+#pragma unroll
+      for (int i0 = 0; i0 < 8; i0 += 4) {
+        u32x4 v[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ih = row0 - 1 + pr, iw = pc - 1;
+          ok[u] = (i0 + u) * 64 + q0 < PP && (unsigned)ih < (unsigned)p.IH &&
+                  (unsigned)iw < (unsigned)p.IW;
+          if (ok[u]) v[u] = *(const u32x4*)(base + (i0 + u) * NT * 8);
+          pr += DR;
+          pc += DC;
+          if (pc >= PW) { pc -= PW; ++pr; }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (ok[u]) *(u32x4*)(base + (i0 + u) * NT * 8) = affine_relu8_pk(v[u], sc, sh, relu);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    EpiBatch<epi_unr<BM, BN, NT>()> pre;
+    if (epi_prefetch<EPI>()) epi_load_batch<BM, BN, NT, EPI>(p, m0, 0, 0, pre);
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          af[fm] = *(const bf16x8*)(smem + cur * PBYTES + aoff[kt][ks][fm]);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          bfr[fn] = *(const bf16x8*)(smem + kt * (BN * 64 * 2) + boff[ks][fn]);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn)
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+      }
+    }
+    // every wave done reading this patch before the epilogue stages the C tile over it (raw
+    // barrier: the next patch's DMA stays in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, (char*)P, m0, 0, t,
+                                            epi_prefetch<EPI>() ? &pre : nullptr);
+  };
+  for (int t = t_beg; t < t_end; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < t_end) tile(t + 1, std::integral_constant<int, 1>{});
+  }
 }
 
 // ------------------------------------------------------------------------------------ wgrad
@@ -1876,20 +2093,38 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
       const int img = (t * 256) / OHW;
       const int row0 = (t * 256 - img * OHW) >> lg;
       const int pseg = (t * 256) / p.pro_seg_rows;  // tiles never straddle a segment (host)
-      const float* psc = Tb + pseg * 2 * B;
-      const float* psh = psc + B;
-      for (int c = tid; c < PP * 8; c += 576) {
-        const int q = c >> 3, pc8 = c & 7;
-        const int pr = q / PW, pc = q - pr * PW;
-        const int ih = row0 - 1 + pr, iw = pc - 1;
-        if ((unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
-          const int ch = tr_swz<B>(q, pc8 * 8);  // within the block's 64-channel slice
-          const float4 s0 = *(const float4*)(psc + ch), s1 = *(const float4*)(psc + ch + 4);
-          const float4 h0 = *(const float4*)(psh + ch), h1 = *(const float4*)(psh + ch + 4);
-          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-          u32x4* ptr = (u32x4*)(Pm + q * B + pc8 * 8);
-          *ptr = affine_relu8(*ptr, sc, sh, true, p.pro_relu != 0);
+      // the first 512 threads walk the patch 64 pixels apart: q & 63 stays fixed per thread, so
+      // does the tr_swz-mapped channel chunk of its slot (the swizzle keys on row bits 1 and 3)
+      // — its 8 scale / shift pairs come from the LDS table once per tile, the pixel walk is
+      // incremental, and four chunks' LDS reads are issued before the first write-back
+      if (tid < 512) {
+        const int q0 = tid >> 3, pc8 = tid & 7;
+        const int ch = tr_swz<B>(q0, pc8 * 8);  // within the block's 64-channel slice
+        const float4* ps = (const float4*)(Tb + pseg * 2 * B + ch);
+        const float4* ph = (const float4*)(Tb + pseg * 2 * B + B + ch);
+        const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
+        const f32x2 sc[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
+        const f32x2 sh[4] = {{h0.x, h0.y}, {h0.z, h0.w}, {h1.x, h1.y}, {h1.z, h1.w}};
+        const int dr = 64 / PW, dc = 64 - dr * PW;
+        int pr = q0 / PW, pc = q0 - pr * PW;
+        uint16_t* base = Pm + tid * 8;  // chunk i at base + i·512·8
+        const bool relu = p.pro_relu != 0;
+        for (int i0 = 0; i0 * 64 + q0 < PP; i0 += 4) {
+          u32x4 v[4];
+          bool ok[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int ih = row0 - 1 + pr, iw = pc - 1;
+            ok[u] = (i0 + u) * 64 + q0 < PP && (unsigned)ih < (unsigned)p.IH &&
+                    (unsigned)iw < (unsigned)p.IW;
+            if (ok[u]) v[u] = *(const u32x4*)(base + (i0 + u) * 4096);
+            pr += dr;
+            pc += dc;
+            if (pc >= PW) { pc -= PW; ++pr; }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (ok[u]) *(u32x4*)(base + (i0 + u) * 4096) = affine_relu8_pk(v[u], sc, sh, relu);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2126,6 +2361,40 @@ void launch_patch(const IgemmArgs& a, hipStream_t s) {
   }
 }
 
+template <int EPI, int PRO>
+void launch_ppatch_t(const IgemmArgs& a0, hipStream_t s) {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  IgemmArgs a = a0;
+  a.nMb = a.M / 256;
+  a.nNb = 1;
+  const int grid = a.nMb < ncu ? a.nMb : ncu;  // one resident block per CU (LDS-bound)
+  hipLaunchKernelGGL((igemm_ppatch<EPI, PRO>), dim3(grid), dim3(512), PP_LDS, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+void launch_ppatch(const IgemmArgs& a, hipStream_t s) {
+  const bool pro = a.pro_sc != nullptr;
+  switch (a.epi_mode) {
+    case 1: pro ? launch_ppatch_t<1, 1>(a, s) : launch_ppatch_t<1, 0>(a, s); break;
+    case 2: pro ? launch_ppatch_t<2, 1>(a, s) : launch_ppatch_t<2, 0>(a, s); break;
+    case 3: pro ? launch_ppatch_t<3, 1>(a, s) : launch_ppatch_t<3, 0>(a, s); break;
+    case 4:
+      if (a.stats2 != nullptr)
+        pro ? launch_ppatch_t<5, 1>(a, s) : launch_ppatch_t<5, 0>(a, s);
+      else
+        pro ? launch_ppatch_t<4, 1>(a, s) : launch_ppatch_t<4, 0>(a, s);
+      break;
+    default: pro ? launch_ppatch_t<0, 1>(a, s) : launch_ppatch_t<0, 0>(a, s); break;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int NST = 2>
 void launch_glds(const IgemmArgs& a, hipStream_t s) {
   if (a.pro_d != nullptr) {  // BN-backward prologue (PRO 2): plain or mode-3 epilogue
@@ -2255,13 +2524,15 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
                                   {256, 256}, {256, 128}, {256, 64}, {128, 128}, {128, 256},
                                   {256, 128}, {128, 128}, {128, 256},
                                   {256, 64}, {256, 128},
-                                  {256, 64}, {128, 256}, {256, 128}};
+                                  {256, 64}, {128, 256}, {256, 128},
+                                  {256, 64}};
 constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
 constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
 constexpr int IG_PATCH0 = 15;  // 3x3 stride-1 kernel with an LDS-resident input patch
 constexpr int IG_GLDS8W = 17;  // 2-stage LDS-DMA, 256 x 64 tile on 8 waves (memory-bound 1x1)
 // 18, 19: 2-stage LDS-DMA, one wave column (WN = 1): the BN-apply prologue runs on the A
 // fragments in registers (the short-K 1x1 expansion convs, conv3 of a bottleneck)
+constexpr int IG_PPATCH = 20;  // persistent 3x3 patch kernel, resident weights (C = N = 64, 32x32)
 // variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
 // {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
 // that many blocks; every split costs an fp32 N x K slab written here and re-read by the
@@ -2558,13 +2829,18 @@ bool igemm_dual_ok(int v, const ConvGeom& g) {
   return lds <= 160 * 1024;
 }
 
-bool igemm_variant_is_patch(int v) { return v >= IG_PATCH0 && v < IG_GLDS8W; }
+bool igemm_ppatch_ok(const ConvGeom& g) {
+  return igemm_patch_ok(g) && g.C == 64 && g.N == 64 && g.OW == 32;
+}
+
+bool igemm_variant_is_patch(int v) { return (v >= IG_PATCH0 && v < IG_GLDS8W) || v == IG_PPATCH; }
 
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
   // patch kernel: BN-apply prologue but no BN-backward one
   if (v >= IG_PATCH0 && v < IG_GLDS8W) return !bn_bwd_pro && igemm_patch_ok(g);
+  if (v == IG_PPATCH) return !bn_bwd_pro && igemm_ppatch_ok(g);
   if (v >= IG_GLDS3 && v < IG_PATCH0 && (pro || bn_bwd_pro)) return false;
   if (bn_bwd_pro) {  // PRO 2 stages dY and x: doubled A staging + a 3 x C table must fit
     const int BM = IG_VARIANTS[v][0], BN = IG_VARIANTS[v][1];
@@ -2622,6 +2898,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 17: launch_glds<256, 64, 8, 1>(a, s); break;
     case 18: launch_glds<128, 256, 4, 1>(a, s); break;
     case 19: launch_glds<256, 128, 8, 1>(a, s); break;
+    case 20: launch_ppatch(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;

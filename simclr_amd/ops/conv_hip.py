@@ -48,6 +48,8 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
         return hit
     cands = []
     for v in range(ops.igemm_nvariants()):
+        if v in _IG_SKIP:
+            continue
         bm = ops.igemm_variant_bm(v)
         if dual is not None:
             if not ops.igemm_dual_ok(v, geom):
@@ -153,6 +155,10 @@ def _parse_variants(spec):
     return out
 
 
+# SIMCLR_IGEMM_SKIP="v,...": leave these conv tile variants out of the autotuner's candidates
+# (A/B experiments, e.g. 20 = the persistent layer1 3x3 kernel)
+_IG_SKIP = frozenset(int(v) for v in os.environ.get("SIMCLR_IGEMM_SKIP", "").split(",")
+                     if v.strip().isdigit())
 # SIMCLR_WGRAD_VARIANTS="lo-hi,...": autotune the weight gradients over these variants only
 # (attribution experiments: register-staged vs LDS-DMA tiles beside the dgrad chain)
 _WG_ONLY = _parse_variants(os.environ.get("SIMCLR_WGRAD_VARIANTS", ""))

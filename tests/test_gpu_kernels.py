@@ -424,6 +424,63 @@ def test_igemm_glds_variants(ops, k, s, p, C, Co, H):
             assert _rel(st, s0) < 1e-3, (v, mode)
 
 
+@pytest.mark.parametrize("N", [160, 8])
+def test_igemm_persistent_patch(ops, N):
+    """Persistent resident-weight 3x3 kernel (igemm_ppatch, variant 20; ResNet-50 layer1 conv2
+    and its dgrad) with several tiles per block (N=160: 640 tiles over at most one block per CU,
+    so the double-buffered patch, uneven runs and idle blocks are all exercised) against an fp32
+    torch conv (plain + BN statistics, BN-apply prologue) and the per-tile patch kernel (v15) for
+    the BN-backward epilogues (modes 3 / 4)."""
+    from simclr_amd.ops.conv_hip import fwd_geom
+    torch.manual_seed(N)
+    C = Co = 64
+    H = W = 32
+    S = 2
+    V = 20
+    x = _bf(torch.randn(N, C, H, W, device=DEV))
+    w = _bf(torch.randn(Co, C, 3, 3, device=DEV) / (C * 9) ** 0.5)
+    g = fwd_geom(N, H, W, C, H, W, 3, 3, 1, 1, Co)
+    assert ops.igemm_variant_ok(V, g, True, False) and ops.igemm_variant_bm(V) == 256
+    M = N * H * W
+    seg = M // S
+    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    wo = w.permute(0, 2, 3, 1).contiguous()
+    refn = F.conv2d(x.float(), w.float(), None, 1, 1).permute(0, 2, 3, 1)
+    out = torch.empty(N, H, W, Co, device=DEV, dtype=torch.bfloat16)
+    st = torch.empty((M // 256) * 2 * Co, device=DEV)
+    ops.igemm(xn, wo, out, None, st, g, None, None, 0, False, 0, None, None, V)
+    assert _rel(out, refn) < 1e-2
+    of = out.float().reshape(-1, Co)
+    s2 = st.view(M // 256, 2, Co).sum(0)
+    assert _rel(s2[0], of.sum(0)) < 1e-3 and _rel(s2[1], (of * of).sum(0)) < 1e-3
+    # BN-apply + ReLU prologue, per-segment tables
+    sc = (torch.rand(S, C, device=DEV) + 0.5).contiguous()
+    sh = (torch.randn(S, C, device=DEV) * 0.3).contiguous()
+    segi = torch.arange(N, device=DEV) // (N // S)
+    a = _bf(torch.relu(x.float() * sc[segi][:, :, None, None] + sh[segi][:, :, None, None]))
+    refa = F.conv2d(a.float(), w.float(), None, 1, 1).permute(0, 2, 3, 1)
+    ops.igemm(xn, wo, out, None, None, g, sc, sh, seg, True, 0, None, None, V)
+    assert _rel(out, refa) < 1e-2
+    # BN-backward epilogues against the per-tile patch kernel
+    yy = _bf(torch.randn(N, H, W, Co, device=DEV))
+    xa = _bf(torch.randn(N, H, W, Co, device=DEV))
+    r = _bf(torch.randn(N, H, W, Co, device=DEV))
+    mi = torch.cat([torch.randn(S, Co, device=DEV) * 0.2,
+                    torch.rand(S, Co, device=DEV) + 0.5]).reshape(-1).contiguous()
+    ss = torch.cat([torch.rand(S, Co, device=DEV) + 0.5,
+                    torch.randn(S, Co, device=DEV) * 0.3]).reshape(-1).contiguous()
+    for mode, ea, eb, ec in ((3, None, yy, None), (4, r, yy, xa)):
+        outs = []
+        for v in (V, 15):
+            o = torch.empty(N, H, W, Co, device=DEV, dtype=torch.bfloat16)
+            s_ = torch.empty((M // 256) * 2 * Co, device=DEV)
+            ops.igemm(xn, wo, o, None, s_, g, None, None, 0, False, mode, ea, eb, v, ss, mi, seg,
+                      0, 0, ec, None, None, None, None, None, None)
+            outs.append((o, s_.view(M // 256, 2, Co).sum(0)))
+        assert _rel(outs[0][0], outs[1][0]) < 1e-2, mode
+        assert _rel(outs[0][1], outs[1][1]) < 1e-3, mode
+
+
 def test_igemm_glds_dgrad_parity_classes(ops):
     """Stride-2 dgrad parity-class geometry (negative tap step, strided output rows) on the
     LDS-DMA kernel against the register-staged kernel, which the conv tests pin to torch."""

@@ -49,6 +49,22 @@ def main():
                                         S, 17))
         print(f"H={H} C={C}: apply {t_apply:.1f} | fwd patch {t_f0:.1f} -> with prologue {t_f1:.1f}"
               f" | wgrad patch {t_w0:.1f} -> with prologue {t_w1:.1f} us", flush=True)
+        if C == 64:  # persistent resident-weight kernel (variant 20)
+            t_p0 = timeit(lambda: ops.igemm(xb, w, out, None, None, g, None, None, 0, False, 0,
+                                            None, None, 20))
+            t_p1 = timeit(lambda: ops.igemm(x, w, out, None, None, g, ss[0], ss[1], M // S, True,
+                                            0, None, None, 20))
+            st = torch.empty((M // 256) * 2 * C, device=dev)
+            mi = torch.cat([torch.zeros(S, C, device=dev), torch.ones(S, C, device=dev)]).reshape(-1)
+            sv = ss.reshape(-1)
+            res = {}
+            for v in (15, 20):
+                res[v] = timeit(lambda: ops.igemm(xb, w, out, None, st, g, None, None, 0, False, 3,
+                                                  None, x, v, sv, mi, M // S, 0, 0, None, None,
+                                                  None, None, None, None, None))
+            print(f"  persistent v20: fwd {t_p0:.1f} (v15 {t_f0:.1f}) | with prologue {t_p1:.1f}"
+                  f" (v15 {t_f1:.1f}) | mode-3 dgrad epilogue v20 {res[20]:.1f} vs v15 "
+                  f"{res[15]:.1f} us", flush=True)
 
 
 if __name__ == "__main__":
