@@ -2012,13 +2012,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
 // B rows of tap (kh, kw) are the pixels (r + kh, c + kw)).  iters_per_split counts 256-row tiles.
 // Host guarantees (wgrad_variant_ok): igemm_patch_ok geometry, N % 64 == 0, no dY prologue;
 // PRO: the X operand's BN-apply + ReLU on the landed patch (256-row tiles inside one segment).
-template <bool PRO>
+#define TR_PTR(a) ((__attribute__((address_space(3))) i16x4*)(uintptr_t)(a))
+template <bool PRO, int OW>
 __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
   constexpr int B = 64;  // co and ci tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int C = p.C, OW = p.OW;
-  const int lg = OW == 32 ? 5 : 4;
-  const int TR = 256 / OW, PW = OW + 2, PP = (TR + 2) * PW;
+  const int C = p.C;
+  constexpr int LG = OW == 32 ? 5 : 4, lg = LG;
+  constexpr int TR = 256 / OW, PW = OW + 2, PP = (TR + 2) * PW;
   const int pinstr = (PP + 7) / 8;                 // 8 patch pixels (128 B each) per DMA
   const int stage = 256 * B + pinstr * 512;        // elements per stage: dY tile + patch
   uint16_t* S0 = (uint16_t*)smem;
@@ -2080,6 +2081,31 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
   const int kh = wid / 3, kw = wid - (wid / 3) * 3;
   const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
   typedef short i16x8 __attribute__((ext_vector_type(8)));
+  // Fragment byte offsets within a stage, fixed for every tile and k-step.  A lane's two row
+  // reads (h = 0, 1) are tile rows ks·32 + o, o = 8g + qq + 4h.  tr_swz<64> of row r and column
+  // 16f + 4pp is chunk (f ^ key(r))·32 + pp·8 bytes, key(r) from r's bits 1 and 3, so
+  //   dY: r·128 + (f ^ key)·32 + pp·8 = ks·4096 + [o·128 + pp·8 + key(o)·32] ^ (f·32)
+  //   patch: pixel q = qb + ks·DQ (DQ = PW, or 2·PW at OW 16): q·128 + ... with the key of the
+  //   shifted pixel, kept as a 2-bit-per-k-step table — instead of ~90 VALU of index math per
+  //   k-step (5-6 per MFMA, the loop's real limit) it is ~16.
+  constexpr int DQ = OW == 32 ? PW : 2 * PW;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(const void, smem);
+  uint32_t dv[2], pv[2], kmask[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int o = 8 * g + qq + 4 * h;
+    const int kd = ((o >> 1) & 1) ^ (((o >> 3) & 1) << 1);
+    dv[h] = (uint32_t)(o * 128 + pp * 8 + kd * 32);
+    const int qb = ((o >> LG) + kh) * PW + (o & (OW - 1)) + kw;
+    pv[h] = (uint32_t)(qb * 128 + pp * 8);
+    uint32_t km = 0;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int q = qb + ks * DQ;
+      km |= (uint32_t)(((q >> 1) & 1) ^ (((q >> 3) & 1) << 1)) << (2 * ks);
+    }
+    kmask[h] = km;
+  }
   if (t_beg < t_end) issue(t_beg, 0);
   for (int t = t_beg; t < t_end; ++t) {
     const int cur = (t - t_beg) & 1;
@@ -2109,11 +2135,12 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
         int pr = q0 / PW, pc = q0 - pr * PW;
         uint16_t* base = Pm + tid * 8;  // chunk i at base + i·512·8
         const bool relu = p.pro_relu != 0;
-        for (int i0 = 0; i0 * 64 + q0 < PP; i0 += 4) {
-          u32x4 v[4];
-          bool ok[4];
+        // two chunks per batch: this 9-wave kernel runs at the 170-VGPR cap of 3 waves / SIMD
+        for (int i0 = 0; i0 * 64 + q0 < PP; i0 += 2) {
+          u32x4 v[2];
+          bool ok[2];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < 2; ++u) {
             const int ih = row0 - 1 + pr, iw = pc - 1;
             ok[u] = (i0 + u) * 64 + q0 < PP && (unsigned)ih < (unsigned)p.IH &&
                     (unsigned)iw < (unsigned)p.IW;
@@ -2123,38 +2150,46 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
             if (pc >= PW) { pc -= PW; ++pr; }
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+          for (int u = 0; u < 2; ++u)
             if (ok[u]) *(u32x4*)(base + (i0 + u) * 4096) = affine_relu8_pk(v[u], sc, sh, relu);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
-    const uint16_t* D = S0 + cur * stage;
-    const uint16_t* P = D + 256 * B;
-#pragma unroll 2
+    // this stage's LDS byte address (a multiple of 1 KiB: it leaves the swizzle bits 5-6 of the
+    // fragment offsets alone, so base + (v ^ c) == (base + v) ^ c)
+    const uint32_t sb = lds0 + (uint32_t)(cur * stage * 2);
+    uint32_t dvt[2], pvt[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      dvt[h] = sb + dv[h];
+      pvt[h] = sb + pv[h];
+    }
+#pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
-      const int r1 = ks * 32 + 8 * g + qq, r2 = r1 + 4;
-      const int q1 = ((r1 >> lg) + kh) * PW + (r1 & (OW - 1)) + kw;
-      const int q2 = ((r2 >> lg) + kh) * PW + (r2 & (OW - 1)) + kw;
       bf16x8 af[4], bfr[4];
+      // dY rows ks·32 + o: ks·4096 B is an immediate; fragment fm sits at chunk (fm ^ key)
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
-        const int col = fm * 16 + 4 * pp;
         i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, D + r1 * B + tr_swz<B>(r1, col)));
+            TR_PTR((dvt[0] ^ (uint32_t)(fm * 32)) + (uint32_t)(ks * 4096)));
         i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, D + r2 * B + tr_swz<B>(r2, col)));
+            TR_PTR((dvt[1] ^ (uint32_t)(fm * 32)) + (uint32_t)(ks * 4096)));
         i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[fm] = __builtin_bit_cast(bf16x8, v);
       }
+      // patch pixels qb + ks·DQ: the shift is an immediate, the swizzle key of the shifted pixel
+      // comes from the per-lane 2-bit table
+      uint32_t pk[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) pk[h] = pvt[h] | (((kmask[h] >> (2 * ks)) & 3u) << 5);
 #pragma unroll
       for (int fn = 0; fn < 4; ++fn) {
-        const int col = fn * 16 + 4 * pp;
         i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, P + q1 * B + tr_swz<B>(q1, col)));
+            TR_PTR((pk[0] ^ (uint32_t)(fn * 32)) + (uint32_t)(32768 + ks * DQ * 128)));
         i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(i16x4, P + q2 * B + tr_swz<B>(q2, col)));
+            TR_PTR((pk[1] ^ (uint32_t)(fn * 32)) + (uint32_t)(32768 + ks * DQ * 128)));
         i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[fn] = __builtin_bit_cast(bf16x8, v);
       }
@@ -2817,7 +2852,8 @@ bool igemm_patch_ok(const ConvGeom& g) {
 // block-output prologue (PRO 3): 2-stage LDS-DMA tiles whose doubled A staging fits the LDS,
 // on 1x1 / stride-1 / unpadded / direct-output convolutions (A row m = output row m)
 bool igemm_dual_ok(int v, const ConvGeom& g) {
-  if (!((v >= IG_GLDS0 && v < IG_GLDS3) || v >= IG_GLDS8W) || !igemm_glds_ok(g, true, false))
+  if (!((v >= IG_GLDS0 && v < IG_GLDS3) || (v >= IG_GLDS8W && v < IG_PPATCH)) ||
+      !igemm_glds_ok(g, true, false))
     return false;
   const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
                       g.OWp == g.OW;
@@ -3026,10 +3062,18 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
       const int pp = (256 / a.OW + 2) * (a.OW + 2);
       const size_t lds = (size_t)2 * (256 * 64 + (pp + 7) / 8 * 512) * 2 +
                          (a.pro_sc != nullptr ? (size_t)2 * 2 * 64 * 4 : 0);
-      if (a.pro_sc != nullptr)
-        hipLaunchKernelGGL(wgrad_patch<true>, dim3(a.nCo * a.nKk * a.splits), dim3(576), lds, s, a);
-      else
-        hipLaunchKernelGGL(wgrad_patch<false>, dim3(a.nCo * a.nKk * a.splits), dim3(576), lds, s, a);
+      const dim3 grid(a.nCo * a.nKk * a.splits);
+      if (a.OW == 32) {
+        if (a.pro_sc != nullptr)
+          hipLaunchKernelGGL((wgrad_patch<true, 32>), grid, dim3(576), lds, s, a);
+        else
+          hipLaunchKernelGGL((wgrad_patch<false, 32>), grid, dim3(576), lds, s, a);
+      } else {
+        if (a.pro_sc != nullptr)
+          hipLaunchKernelGGL((wgrad_patch<true, 16>), grid, dim3(576), lds, s, a);
+        else
+          hipLaunchKernelGGL((wgrad_patch<false, 16>), grid, dim3(576), lds, s, a);
+      }
       HIP_CHECK_LAUNCH();
       break;
     }

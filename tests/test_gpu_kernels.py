@@ -424,7 +424,7 @@ def test_igemm_glds_variants(ops, k, s, p, C, Co, H):
             assert _rel(st, s0) < 1e-3, (v, mode)
 
 
-@pytest.mark.parametrize("N", [160, 8])
+@pytest.mark.parametrize("N", [160, 8, 1024])
 def test_igemm_persistent_patch(ops, N):
     """Persistent resident-weight 3x3 kernel (igemm_ppatch, variant 20; ResNet-50 layer1 conv2
     and its dgrad) with several tiles per block (N=160: 640 tiles over at most one block per CU,
