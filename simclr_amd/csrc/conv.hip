@@ -770,7 +770,7 @@ __host__ __device__ constexpr size_t igemm_glds_pro_offset(int BM, int BN, int N
 // NST == 3: three LDS stages; the DMA of tile k+2 is issued while tile k computes and a
 // counted vmcnt keeps tile k+1's DMA in flight across the (raw) barrier.
 template <int BM, int BN, int WM, int WN, int PRO, int EPI, int NST>
-__global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
+__global__ __launch_bounds__(64 * WM * WN, NST == 1 ? 2 : 1) void igemm_glds(IgemmArgs p) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -907,7 +907,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
   issue(0, 0);
   if (NST == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = NST == 3 ? kt % 3 : kt & 1;
+    const int cur = NST == 3 ? kt % 3 : NST == 2 ? (kt & 1) : 0;
     if (NST == 3 && kt + 1 < nk)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // tile kt+1 stays in flight
     else if (PRO == 3 && nb == 0 && kt > 0)
@@ -920,7 +920,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
     // raw barrier (__syncthreads() would drain the in-flight DMA): tile kt visible to every
     // wave, every wave done reading the buffer the next issue overwrites
     __builtin_amdgcn_s_barrier();
-    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    if (NST > 1 && kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
     // prologue passes over the landed tile: chunk c = tid + i·NT sits in row c / 8 and holds
     // logical channel chunk (c % 8) ^ (row % 8), the same for every i (NT % 64 == 0), so the
     // per-channel tables are read from LDS once per k-tile rather than once per chunk (LDS
@@ -1050,6 +1050,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_glds(IgemmArgs p) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
+    }
+    if constexpr (NST == 1) {
+      // single stage (the short-K tiles that run 2 blocks per CU: the other block's MFMAs
+      // cover this one's loads and epilogue): every wave done with the tile, then refill it
+      if (kt + 1 < nk) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(kt + 1, 0);
+      }
     }
   }
   __syncthreads();  // the epilogue reuses the staging LDS
@@ -2454,7 +2463,7 @@ void launch_glds(const IgemmArgs& a, hipStream_t s) {
     return;
   }
   if (a.pro_sc != nullptr) {
-    if constexpr (NST == 2) {  // the 3-stage tiles leave no LDS for the prologue table
+    if constexpr (NST <= 2) {  // the 3-stage tiles leave no LDS for the prologue table
       switch (a.epi_mode) {
         case 1: launch_glds_t<BM, BN, WM, WN, 1, 1, NST>(a, s); break;
         case 2: launch_glds_t<BM, BN, WM, WN, 1, 2, NST>(a, s); break;
@@ -2560,7 +2569,7 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
                                   {256, 128}, {128, 128}, {128, 256},
                                   {256, 64}, {256, 128},
                                   {256, 64}, {128, 256}, {256, 128},
-                                  {256, 64}};
+                                  {256, 64}, {128, 256}, {256, 128}};
 constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
 constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
 constexpr int IG_PATCH0 = 15;  // 3x3 stride-1 kernel with an LDS-resident input patch
@@ -2568,6 +2577,9 @@ constexpr int IG_GLDS8W = 17;  // 2-stage LDS-DMA, 256 x 64 tile on 8 waves (mem
 // 18, 19: 2-stage LDS-DMA, one wave column (WN = 1): the BN-apply prologue runs on the A
 // fragments in registers (the short-K 1x1 expansion convs, conv3 of a bottleneck)
 constexpr int IG_PPATCH = 20;  // persistent 3x3 patch kernel, resident weights (C = N = 64, 32x32)
+// 21, 22: single-stage LDS-DMA tiles, 2 blocks per CU (short-K 1x1 convs: one block's loads and
+// epilogue under the other's MFMAs instead of a second LDS stage); BN-apply prologue only
+constexpr int IG_GLDS1 = 21;
 // variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
 // {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
 // that many blocks; every split costs an fp32 N x K slab written here and re-read by the
@@ -2877,6 +2889,7 @@ bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   // patch kernel: BN-apply prologue but no BN-backward one
   if (v >= IG_PATCH0 && v < IG_GLDS8W) return !bn_bwd_pro && igemm_patch_ok(g);
   if (v == IG_PPATCH) return !bn_bwd_pro && igemm_ppatch_ok(g);
+  if (v >= IG_GLDS1) return !bn_bwd_pro && igemm_glds_ok(g, pro, false);
   if (v >= IG_GLDS3 && v < IG_PATCH0 && (pro || bn_bwd_pro)) return false;
   if (bn_bwd_pro) {  // PRO 2 stages dY and x: doubled A staging + a 3 x C table must fit
     const int BM = IG_VARIANTS[v][0], BN = IG_VARIANTS[v][1];
@@ -2935,6 +2948,8 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 18: launch_glds<128, 256, 4, 1>(a, s); break;
     case 19: launch_glds<256, 128, 8, 1>(a, s); break;
     case 20: launch_ppatch(a, s); break;
+    case 21: launch_glds<128, 256, 2, 2, 1>(a, s); break;
+    case 22: launch_glds<256, 128, 2, 2, 1>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
