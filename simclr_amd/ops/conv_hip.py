@@ -159,8 +159,14 @@ def _parse_variants(spec):
 # (A/B experiments, e.g. 20 = the persistent layer1 3x3 kernel)
 _IG_SKIP = frozenset(int(v) for v in os.environ.get("SIMCLR_IGEMM_SKIP", "").split(",")
                      if v.strip().isdigit())
-# the single-stage 2-blocks-per-CU short-K tiles (21, 22) are opt-in until their end-to-end
-# golden-run check (SIMCLR_IGEMM_SHORTK=1)
+# Opt-in tile variants (profiles/r3_optimization_log.md): the persistent layer1 3x3 kernel (20,
+# SIMCLR_IGEMM_PPATCH=1; end to end neutral) and the single-stage 2-blocks-per-CU short-K tiles
+# (21, 22, SIMCLR_IGEMM_SHORTK=1).  Both are correct per launch (kernel tests), but their
+# epilogues sum the BatchNorm partials in another order, and the ResNet-50 batch-128 golden run
+# (tests/test_gpu_e2e.py) then drifted past its bounds in 2 of 2 runs each (0.16-0.27 running-mean
+# loss difference vs 0.115 without): off by default until that is understood.
+if os.environ.get("SIMCLR_IGEMM_PPATCH", "0") != "1":
+    _IG_SKIP = _IG_SKIP | {20}
 if os.environ.get("SIMCLR_IGEMM_SHORTK", "0") != "1":
     _IG_SKIP = _IG_SKIP | {21, 22}
 # SIMCLR_WGRAD_VARIANTS="lo-hi,...": autotune the weight gradients over these variants only
