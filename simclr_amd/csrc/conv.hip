@@ -1816,7 +1816,7 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 // counted vmcnt keeps step it+1's DMA in flight across the barrier (raw s_barrier: hipcc's
 // __syncthreads() would drain it with vmcnt(0)) — for the HBM-bound 1x1 weight gradients.
 template <int BCO, int BKK, int WM, int WN, bool PRO, int NST>
-__global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
+__global__ __launch_bounds__(64 * WM * WN, NST == 1 ? 2 : 1) void wgrad_glds(WgradArgs p) {
   constexpr int NW = WM * WN;
   constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = 64 / (RPD * NW);
   constexpr int CPX = BKK / 8, RPX = 64 / CPX, XI = 64 / (RPX * NW);
@@ -1945,14 +1945,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
   if (nit > 0) issue(0, 0);
   if (NST == 3 && nit > 1) issue(1, 1);
   for (int it = 0; it < nit; ++it) {
-    const int cur = NST == 3 ? it % 3 : it & 1;
+    const int cur = NST == 3 ? it % 3 : NST == 2 ? (it & 1) : 0;
     if (NST == 3 && it + 1 < nit)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step it+1 stays in flight
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // step it landed for every wave; buffer (it-1) % NST is free
-    if (it + NST - 1 < nit) issue(it + NST - 1, (it + NST - 1) % NST);
+    if (NST > 1 && it + NST - 1 < nit) issue(it + NST - 1, (it + NST - 1) % NST);
     if (PRO && !HOIST) {
       // rows past mend hold zero dY, so whatever the transform makes of them contributes 0;
       // columns past K are dropped by the store
@@ -2006,6 +2006,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
       __builtin_amdgcn_s_barrier();
     }
     wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * BCO, Xs + cur * 64 * BKK, acc);
+    if constexpr (NST == 1) {
+      // single stage, 2 blocks per CU (the other block's MFMAs cover this one's DMA wait):
+      // every wave done reading the tile, then refill it
+      if (it + 1 < nit) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(it + 1, 0);
+      }
+    }
   }
   wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
   const int kb[1] = {k0};
@@ -2569,7 +2578,7 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
                                   {256, 128}, {128, 128}, {128, 256},
                                   {256, 64}, {256, 128},
                                   {256, 64}, {128, 256}, {256, 128},
-                                  {256, 64}, {128, 256}, {256, 128}};
+                                  {256, 64}, {128, 256}, {256, 128}, {128, 128}};
 constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
 constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
 constexpr int IG_PATCH0 = 15;  // 3x3 stride-1 kernel with an LDS-resident input patch
@@ -2590,13 +2599,15 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {64, 256, 512},  {128, 128, 256}, {64, 256, 256},
                                   {128, 64, 512},  {128, 128, 256}, {64, 128, 512},
                                   {256, 128, 256}, {64, 64, 256},
-                                  {64, 128, 768}, {128, 64, 768}};
+                                  {64, 128, 768}, {128, 64, 768},
+                                  {128, 128, 512}, {256, 128, 512}};
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 // wgrad_tn with loads two steps ahead (DEEP): the 64 x 128 / 128 x 64 tiles gain 10-17 % on the
 // 3x3 / 1x1 weight gradients (tools/wgrad_probe.py); the 128 x 128 and 256 x 64 DEEP tiles spill
 // at the 256-VGPR cap of two blocks per CU and lose (not instantiated)
 constexpr int WG_DEEP0 = 18;
+constexpr int WG_GLDS1 = 20;  // 20, 21: single-stage LDS-DMA tiles, 2 blocks per CU
 
 
 // -------------------------------------------------- fused 1x1 backward: dgrad + wgrad in one pass
@@ -2950,6 +2961,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 20: launch_ppatch(a, s); break;
     case 21: launch_glds<128, 256, 2, 2, 1>(a, s); break;
     case 22: launch_glds<256, 128, 2, 2, 1>(a, s); break;
+    case 23: launch_glds<128, 128, 2, 2, 1>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
@@ -2970,10 +2982,11 @@ int igemm_tail_ticket_words(int nNb, int S, int ngrp) { return nNb * S * ngrp + 
 
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
-bool wgrad_variant_glds(int v) { return v >= WG_GLDS0 && v < WG_PATCH0; }
+bool wgrad_variant_glds(int v) { return (v >= WG_GLDS0 && v < WG_PATCH0) || v >= WG_GLDS1; }
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
   if (v == WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
+  if (v >= WG_GLDS1) return !dy_pro && igemm_glds_ok(g, pro, false);
   if (v >= WG_DEEP0) return true;  // register-staged: every prologue
   // wgrad_glds has the X-operand BN-apply prologue only (no dY BN-backward prologue)
   return v < WG_GLDS0 || (!dy_pro && igemm_glds_ok(g, pro, false));
@@ -3094,6 +3107,8 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     }
     case 18: launch_wgrad<64, 128, 2, 2, true>(a, s); break;
     case 19: launch_wgrad<128, 64, 2, 2, true>(a, s); break;
+    case 20: launch_wgrad_glds<128, 128, 2, 2, 1>(a, s); break;
+    case 21: launch_wgrad_glds<256, 128, 2, 2, 1>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;
