@@ -167,6 +167,12 @@ _IG_SKIP = frozenset(int(v) for v in os.environ.get("SIMCLR_IGEMM_SKIP", "").spl
 # faster expansion / reduction 1x1 convs, golden run within bounds in 2 of 2 runs.
 if os.environ.get("SIMCLR_IGEMM_PPATCH", "0") != "1":
     _IG_SKIP = _IG_SKIP | {20}
+# the single-stage 128 x 128 forward tile (23) and weight-gradient tiles (wgrad 20, 21): end to
+# end neutral, and with them in the candidate set the golden run drifted to 0.124 (bound 0.12):
+# opt-in (SIMCLR_TILES_EXTRA=1)
+_EXTRA = os.environ.get("SIMCLR_TILES_EXTRA", "0") == "1"
+if not _EXTRA:
+    _IG_SKIP = _IG_SKIP | {23}
 if os.environ.get("SIMCLR_IGEMM_SHORTK", "1") == "0":
     _IG_SKIP = _IG_SKIP | {21, 22}
 # SIMCLR_WGRAD_VARIANTS="lo-hi,...": autotune the weight gradients over these variants only
@@ -225,7 +231,8 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
     v = tuning.cached(key)
     if v is None:
         cands = [v for v in range(ops.wgrad_nvariants())
-                 if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)]
+                 if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)
+                 and (_EXTRA or v < 20)]
         if _WG_ONLY is not None:  # experiment: restrict the candidates (fallback: all)
             cands = [v for v in cands if v in _WG_ONLY] or cands
         v = tuning.pick(key, cands, 1 if N <= 64 else 0,
