@@ -144,7 +144,16 @@ def test_golden_trajectory_resnet50_batch128_60_steps():
     assert t_hip.hip and not t_ref.hip
     with torch.no_grad():
         t_ref.store.master.copy_(t_hip.store.master)
-    l_hip = [float(t_hip.step(x).item()) for x in xs]
+    # fixed tile variants (autotuner off, as under runtime.deterministic): the 60-step trajectory
+    # is sensitive to the fp32 summation order of whichever tiles win the timing near-ties on a
+    # given box (profiles/r3_optimization_log.md); pinned, the HIP side is the same on every box
+    from simclr_amd.ops import tuning
+    was = tuning.ENABLED
+    tuning.set_enabled(False)
+    try:
+        l_hip = [float(t_hip.step(x).item()) for x in xs]
+    finally:
+        tuning.set_enabled(was)
     l_ref = [float(t_ref.step(x).item()) for x in xs]
     diffs = [abs(a - b) for a, b in zip(l_hip, l_ref)]
     print("hip", [round(v, 3) for v in l_hip])
