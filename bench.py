@@ -51,8 +51,10 @@ def self_launch(args, argv) -> int:
     WORLD_SIZE / MASTER_* in their environment) and return the first non-zero exit code (the
     survivors are terminated) or 0.  Runs before any GPU call in this process; rank 0's JSON
     line reaches stdout directly."""
-    from simclr_amd.runtime.launcher import launch, parse_args
-    ndev = torch.cuda.device_count()  # counts devices without initialising HIP in this process
+    from simclr_amd.runtime.launcher import launch, parse_args, visible_gpu_count
+    # visibility variables / KFD topology only: this parent forks every rank and must never
+    # initialise HIP itself (torch.cuda.device_count() can fall back to hipGetDeviceCount)
+    ndev = visible_gpu_count()
     if ndev and ndev < args.gpus and os.environ.get("SIMCLR_DIST_BACKEND") != "gloo":
         raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} GPU(s) visible")
     la = parse_args(["--nproc_per_node", str(args.gpus), "--master_addr", "127.0.0.1",
@@ -113,7 +115,9 @@ def run_ours(args, rank, world, dev):
     pstate.make_stat_group(st)
     if st.comm and dev.type == "cuda":
         from simclr_amd.comm import setup_stats_exchange
-        setup_stats_exchange(st, dev)  # IPC BatchNorm statistics (self-tested, else RCCL)
+        # IPC BatchNorm statistics as a CANDIDATE (self-tested, else RCCL): the probe below
+        # times it against RCCL and keeps the faster; training defaults to RCCL
+        setup_stats_exchange(st, dev, mode=os.environ.get("SIMCLR_BN_COMM", "auto"))
     ov = [f"experiment.base_cnn={args.model}", f"experiment.batches={args.batch}",
           f"model.cifar_stem={'true' if args.cifar_stem else 'null'}",
           "data.synthetic=true", f"runtime.precision={args.precision}",
@@ -121,7 +125,10 @@ def run_ours(args, rank, world, dev):
           f"runtime.bucket_mb={args.bucket_mb}"]
     cfg = task_config(compose(str(CONF_DIR), "config", ov, job_name="bench"))
     seed_everything(cfg["parameter"]["seed"])
-    n_img = max(8192, args.batch * world * 2)
+    # CIFAR-10's training-set length at every N: at N = 8 an epoch is 12 steps, as
+    # in the reference; each rank's shard order is uploaded without a stream sync at rollover
+    # (ImageNet-shape runs keep a smaller set: 50,000 224² images would be 7.5 GB of host RAM)
+    n_img = 50000 if args.size <= 64 else max(8192, 4 * args.batch * world)
     ds = synthetic_dataset(n_img, 10, size=args.size, seed=rank)
     loader = ContrastiveLoader(ds, args.batch, dev, rank=rank, world=world,
                                strength=cfg["experiment"]["strength"], seed=7, views=2)

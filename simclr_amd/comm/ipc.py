@@ -161,12 +161,15 @@ class IpcStatsExchange:
 def setup_stats_exchange(st, device: torch.device, mode: Optional[str] = None):
     """Attach an IPC statistics exchange to the parallel state ``st`` when it applies.
 
-    ``mode`` (or ``SIMCLR_BN_COMM``): ``rccl`` never, ``ipc`` always (raise if impossible),
-    ``auto`` (default) at world > 1 over RCCL (one GPU per rank) when the self-test passes on
-    every rank.  ``auto`` skips the gloo rehearsals that put several ranks on ONE GPU: their
-    processes' queues are time-sliced, so every exchange waits for a context switch (correct —
-    tests/test_gpu_distributed.py runs it explicitly — but ~50 ms per BatchNorm)."""
-    mode = (mode or os.environ.get("SIMCLR_BN_COMM", "auto")).lower()
+    ``mode`` (or ``SIMCLR_BN_COMM``): ``rccl`` (the default: the exchange has not yet been
+    validated across two physical GPUs, so training keeps the RCCL statistics all-reduce unless
+    asked), ``ipc`` always (raise if impossible), ``auto`` at world > 1 over RCCL (one GPU per
+    rank) when the self-test passes on every rank — bench.py uses ``auto`` as a candidate that
+    its collective probe times against RCCL.  ``auto`` skips the gloo rehearsals that put several
+    ranks on ONE GPU: their processes' queues are time-sliced, so every exchange waits for a
+    context switch (correct — tests/test_gpu_distributed.py runs it explicitly — but ~50 ms per
+    BatchNorm)."""
+    mode = (mode or os.environ.get("SIMCLR_BN_COMM", "rccl")).lower()
     st.ipc = None
     if mode == "rccl" or not st.comm or st.world_size < 2 or device.type != "cuda":
         if mode == "ipc" and st.world_size > 1 and device.type != "cuda":
@@ -231,16 +234,21 @@ class StepGuard:
 
     * the first ``TUNING_STEPS`` steps run with ``st.ipc`` detached (statistics over RCCL) and
       end with ``tuning.sync_from_rank0`` — identical tiles on every rank;
-    * after every step the exchange's sticky error flag is copied into pinned host memory
-      (async, no sync) and the copy of the previous step is read: ``on_error="raise"`` raises
-      ``IpcExchangeError`` (the fail-fast launcher then stops every rank — training never runs on
-      from partial statistics), ``"defer"`` leaves the check to the caller (bench.py)."""
+    * after every step the exchange's sticky error flag is all-reduced (MAX) across the ranks
+      on the device — a rank whose late arrival made a PEER time out learns of it too — and
+      copied into pinned host memory behind an event; the next step's check waits for that
+      event (the previous step has finished on the device by then; the host stays one step
+      ahead) and reads the flag: ``on_error="raise"`` raises ``IpcExchangeError`` on every rank
+      no later than the step after the timeout (the fail-fast launcher then stops the job —
+      training never runs on from partial statistics), ``"defer"`` leaves the check to the
+      caller (bench.py)."""
 
     def __init__(self, st, on_error: str = "raise"):
         self.st = st
         self.on_error = on_error
         self.eager_steps = 0
-        self._err_host: Optional[torch.Tensor] = None
+        self._pending = None  # (host flag, event or None, step) of the last issued check
+        self._bufs: List[torch.Tensor] = []
 
     def run(self, body, *a):
         if self.eager_steps >= TUNING_STEPS or not self.st.comm:
@@ -256,15 +264,39 @@ class StepGuard:
         tuning.sync_from_rank0(self.st.group)
         return out
 
+    def _land(self) -> None:
+        """Wait for the previously issued flag copy and raise if any rank timed out."""
+        if self._pending is None:
+            return
+        host, ev, s = self._pending
+        self._pending = None
+        if ev is not None:
+            ev.synchronize()
+        if self.on_error == "raise" and int(host[0]) != 0:
+            raise IpcExchangeError(
+                f"rank {self.st.rank}: IPC BatchNorm-statistics exchange timed out on some rank "
+                f"at or before step {s}; stopping (that step's statistics were partial)")
+
     def check(self, step: int = -1) -> None:
         ipc = self.st.ipc
         if ipc is None:
             return
-        if self._err_host is None:
-            self._err_host = torch.zeros(1, dtype=torch.int32,
-                                         pin_memory=ipc.err.is_cuda)
-        elif self.on_error == "raise" and int(self._err_host[0]) != 0:
-            raise IpcExchangeError(
-                f"rank {self.st.rank}: IPC BatchNorm-statistics exchange timed out at or before "
-                f"step {step}; stopping (that step's statistics were partial)")
-        self._err_host.copy_(ipc.err, non_blocking=True)
+        self._land()
+        cuda = ipc.err.is_cuda
+        if not self._bufs:  # two pinned flags: the one being written is never the one read
+            self._bufs = [torch.zeros(1, dtype=torch.int32, pin_memory=cuda) for _ in range(2)]
+        host = self._bufs[step % 2 if step >= 0 else 0]
+        flag = ipc.err.clone()
+        if self.st.comm and dist.is_initialized():
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.st.group)
+        host.copy_(flag, non_blocking=cuda)
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(flag.device))
+        self._pending = (host, ev, step)
+
+    def flush(self, step: int = -1) -> None:
+        """Check the last issued flag now (epoch end, before saving or exiting)."""
+        self.check(step)
+        self._land()

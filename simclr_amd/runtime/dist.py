@@ -41,9 +41,18 @@ def pick_device(local_rank: int, use_cuda: bool = True) -> torch.device:
     return torch.device("cpu")
 
 
+# process-group timeout: a rank that dies or hangs fails every collective of its peers within
+# this bound (the fail-fast launcher then stops the job) instead of holding the node for
+# torch's default 30 minutes; ``runtime.pg_timeout_s`` overrides it
+DEFAULT_PG_TIMEOUT_S = 600.0
+
+
 def init_distributed(cfg=None, use_cuda: bool = True, backend: Optional[str] = None,
-                     timeout_s: float = 1800.0) -> pstate.ParallelState:
+                     timeout_s: Optional[float] = None) -> pstate.ParallelState:
     rank, world, local = resolve_world(cfg)
+    if timeout_s is None:
+        rt = (cfg or {}).get("runtime", {}) if hasattr(cfg or {}, "get") else {}
+        timeout_s = float((rt or {}).get("pg_timeout_s", None) or DEFAULT_PG_TIMEOUT_S)
     device = pick_device(local, use_cuda)
     if world > 1 and not dist.is_initialized():
         be = backend or ("nccl" if device.type == "cuda" else "gloo")

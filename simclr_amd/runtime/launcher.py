@@ -73,6 +73,36 @@ def build_commands(args) -> List[tuple]:
     return out
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_gpu_count(kfd_nodes: str = KFD_NODES) -> Optional[int]:
+    """GPUs a child process will see, WITHOUT initialising HIP in this process (a launcher
+    parent must never touch the GPU: ``torch.cuda.device_count()`` falls back to
+    ``hipGetDeviceCount`` on ROCm when amdsmi is unavailable).  The visibility variables win
+    when set; otherwise the KFD topology's GPU nodes (``simd_count > 0``; CPU nodes have 0) are
+    counted.  None when neither source is available."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([t for t in v.split(",") if t.strip() != ""])
+    try:
+        n = 0
+        for node in sorted(os.listdir(kfd_nodes)):
+            try:
+                with open(os.path.join(kfd_nodes, node, "properties")) as f:
+                    for line in f:
+                        k, _, val = line.partition(" ")
+                        if k == "simd_count" and int(val) > 0:
+                            n += 1
+                            break
+            except (OSError, ValueError):
+                continue
+        return n
+    except OSError:
+        return None
+
+
 def _terminate(procs, grace: float) -> None:
     for p in procs:
         if p.poll() is None:

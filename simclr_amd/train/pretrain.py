@@ -26,6 +26,7 @@ from typing import Optional
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from ..comm.ipc import StepGuard
 from ..config import check_pretrain_conf
@@ -38,7 +39,8 @@ from ..optim.lars import FusedLARS, weight_decay_per_param
 from ..optim.schedule import MODE_WARMUP_COSINE, calculate_initial_lr
 from ..parallel.flat import FlatParamStore
 from ..runtime.dist import init_distributed
-from ..utils.checkpoint import checkpoint_name, save_reference_checkpoint, save_resume, load_resume
+from ..utils.checkpoint import (checkpoint_name, gather_rng_states, load_resume,
+                                save_reference_checkpoint, save_resume)
 from ..utils.misc import cfg_get, seed_everything, MetricsWriter, refuse_experiment_knobs
 
 log = logging.getLogger(__name__)
@@ -232,7 +234,7 @@ def pretrain(cfg) -> dict:
         if st.device.type == "cuda":
             torch.cuda.synchronize()
         dt = max(time.time() - t0, 1e-9)
-        tr.guard.check(step_global)  # the epoch's last step (its flag copy has landed)
+        tr.guard.flush(step_global)  # the epoch's last step (its flag copy has landed)
         imgs = nsteps * cfg["experiment"]["batches"] * st.world_size
         summary.update(epochs_run=summary["epochs_run"] + 1, steps=step_global)
         if rank == 0:
@@ -248,7 +250,13 @@ def pretrain(cfg) -> dict:
                     epoch, cfg["experiment"]["output_model_name"]))
                 if cfg_get(cfg, "runtime.save_resume", True):
                     save_resume("resume-{}.pt".format(epoch), tr.model, tr.opt, epoch,
-                                loader.counter)
+                                loader.counter, group=st.group if st.world_size > 1 else None)
+        elif epoch % save_every == 0 and cfg_get(cfg, "runtime.save_resume", True):
+            gather_rng_states(dst=0, group=st.group)  # rank 0's resume file holds every rank's
+        if st.world_size > 1:
+            # no rank starts the next epoch's first exchange while rank 0 is still logging /
+            # saving (a multi-second save would exceed the IPC exchange's spin bound)
+            dist.barrier(group=st.group)
         if done:
             break
     if prof is not None:

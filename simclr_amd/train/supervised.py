@@ -131,6 +131,7 @@ def supervised(cfg) -> dict:
             guard.check(step)
             if max_steps is not None and step >= max_steps:
                 break
+        guard.flush(step)  # the epoch's last flag copy
         line = None
         if st.rank == 0:
             line = "Epoch:{}/{} progress:{:.3f} loss:{:.3f}, lr:{:.7f}".format(
@@ -156,6 +157,10 @@ def supervised(cfg) -> dict:
                 best_file = checkpoint_name(epoch, cfg["experiment"]["output_model_name"])
                 save_reference_checkpoint(model, best_file)
                 summary["best_checkpoint"] = best_file
+        if st.world_size > 1:
+            # nobody starts the next epoch's first statistics exchange while rank 0 is still
+            # saving (a multi-second save would exceed the IPC exchange's spin bound)
+            dist.barrier()
         if max_steps is not None and step >= max_steps:
             break
     metrics.close()

@@ -71,16 +71,43 @@ def load_into(model: nn.Module, path, strict: bool = False, store=None):
     return missing, unexpected
 
 
+def _local_rng() -> dict:
+    """This process's generators: host torch, its OWN device's CUDA generator, NumPy."""
+    cuda = None
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        cuda = torch.cuda.get_rng_state()
+    return {"torch_rng": torch.get_rng_state(), "cuda_rng_device": cuda,
+            "numpy_rng": _numpy_rng_state()}
+
+
+def gather_rng_states(dst: int = 0, group=None) -> Optional[list]:
+    """Collective: every rank's ``_local_rng()``, as a rank-indexed list on ``dst`` (None on
+    the other ranks).  Call it on every rank when rank ``dst`` saves a resume file."""
+    import torch.distributed as dist
+    mine = _local_rng()
+    if group is None or not dist.is_initialized():
+        return [mine]
+    world = dist.get_world_size(group)
+    out = [None] * world if dist.get_rank(group) == dst else None
+    dist.gather_object(mine, out, dst=dst, group=group)
+    return out
+
+
 def save_resume(path: str, model: nn.Module, optimizer, epoch: int, step: int,
-                extra: Optional[dict] = None) -> None:
+                extra: Optional[dict] = None, group=None) -> None:
+    """Resume file (rank 0 writes it).  ``group``: multi-rank job — every other rank must call
+    ``gather_rng_states(0, group)`` at the same point, so the file holds each rank's own
+    generators (``rank_rng[r]``), restored per rank by ``restore_rng``."""
+    local = _local_rng()
+    ranks = gather_rng_states(0, group) if group is not None else [local]
     torch.save({
         "model": reference_state_dict(model),
         "optimizer": optimizer.state_dict() if optimizer is not None else None,
         "epoch": int(epoch),
         "step": int(step),
-        "torch_rng": torch.get_rng_state(),
-        "cuda_rng": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else [],
-        "numpy_rng": _numpy_rng_state(),
+        "torch_rng": local["torch_rng"],
+        "numpy_rng": local["numpy_rng"],
+        "rank_rng": ranks,
         "extra": extra or {},
     }, path)
 
@@ -93,15 +120,22 @@ def _numpy_rng_state() -> dict:
             "has_gauss": int(has_gauss), "gauss": float(gauss)}
 
 
-def restore_rng(blob: dict) -> None:
-    """Restore the host / device / NumPy generators saved by ``save_resume``."""
+def restore_rng(blob: dict, rank: Optional[int] = None) -> None:
+    """Restore this rank's host / device / NumPy generators saved by ``save_resume``: the
+    ``rank_rng[rank]`` entry (each rank gets its own state back, its device generator on its
+    current device); files without one fall back to the top-level host / NumPy state."""
     import numpy as np
-    if blob.get("torch_rng") is not None:
-        torch.set_rng_state(blob["torch_rng"])
-    cuda = blob.get("cuda_rng") or []
-    if cuda and torch.cuda.is_available() and len(cuda) == torch.cuda.device_count():
-        torch.cuda.set_rng_state_all(cuda)
-    n = blob.get("numpy_rng")
+    import torch.distributed as dist
+    if rank is None:
+        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+    ranks = blob.get("rank_rng") or []
+    ent = ranks[rank] if rank < len(ranks) else blob
+    if ent.get("torch_rng") is not None:
+        torch.set_rng_state(ent["torch_rng"])
+    cuda = ent.get("cuda_rng_device")
+    if cuda is not None and torch.cuda.is_available():
+        torch.cuda.set_rng_state(cuda)
+    n = ent.get("numpy_rng")
     if n:
         np.random.set_state(("MT19937", n["keys"].numpy().astype(np.uint32), n["pos"],
                              n["has_gauss"], n["gauss"]))

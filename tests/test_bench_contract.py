@@ -49,3 +49,49 @@ def test_bench_world_mismatch_is_an_error(tmp_path):
                        timeout=300)
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_self_launch_never_touches_hip(monkeypatch):
+    """The parent that forks every rank counts GPUs from the visibility variables / KFD
+    topology only: torch.cuda.device_count() (which can fall back to hipGetDeviceCount) is never
+    called and HIP stays uninitialised in the parent."""
+    import argparse
+    import torch
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_script", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)  # (the bench/ package shadows the name)
+    spec.loader.exec_module(bench)
+    from simclr_amd.runtime import launcher
+
+    def boom(*a, **k):
+        raise AssertionError("the launcher parent called into torch.cuda")
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setattr(torch.cuda, "is_available", boom)
+    seen = {}
+
+    def fake_launch(la):
+        seen["n"] = la.nproc_per_node
+        return 0
+    monkeypatch.setattr(launcher, "launch", fake_launch)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    rc = bench.self_launch(argparse.Namespace(gpus=8), ["--gpus", "8"])
+    assert rc == 0 and seen["n"] == 8
+    assert not torch.cuda.is_initialized()
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1")
+    with pytest.raises(SystemExit, match="only 2 GPU"):
+        bench.self_launch(argparse.Namespace(gpus=8), ["--gpus", "8"])
+
+
+def test_visible_gpu_count_reads_kfd_topology(tmp_path, monkeypatch):
+    from simclr_amd.runtime.launcher import visible_gpu_count
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    for i, simd in enumerate([0, 1024, 1024, 0]):  # CPU nodes have simd_count 0
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simd}\nmem_banks_count 1\n")
+    assert visible_gpu_count(str(tmp_path)) == 2
+    assert visible_gpu_count(str(tmp_path / "missing")) is None
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert visible_gpu_count(str(tmp_path)) == 0

@@ -82,6 +82,57 @@ def test_step_guard_raises_on_exchange_timeout():
     d.check(1)  # deferred: the caller (bench.py) checks collectively
 
 
+def _guard_worker(rank, world, port, out_dir, s_bad):
+    import os
+    import time
+    import torch
+    import torch.distributed as dist
+    from simclr_amd.comm.ipc import IpcExchangeError, StepGuard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class St:
+        comm = True
+    st = St()
+    st.rank, st.group, st.ipc = rank, dist.group.WORLD, _FakeIpc()
+    g = StepGuard(st)
+    raised_at = -1
+    for step in range(s_bad + 4):
+        def body():
+            if step == s_bad:
+                if rank == 1:
+                    time.sleep(0.5)  # rank 1 arrives late at this step's exchanges ...
+                elif st.ipc is not None:
+                    st.ipc.err.fill_(1)  # ... so rank 0's spin times out (sticky device flag)
+        try:
+            g.run(body)
+            g.check(step)
+        except IpcExchangeError:
+            raised_at = step
+            break
+    with open(os.path.join(out_dir, f"g{rank}"), "w") as f:
+        f.write(str(raised_at))
+    dist.destroy_process_group()
+
+
+def test_step_guard_timeout_raises_on_every_rank_within_one_step(tmp_path, monkeypatch):
+    """A peer's late arrival makes rank 0's exchange time out at step s: EVERY rank (the late
+    one too, which saw no timeout itself) raises IpcExchangeError no later than step s + 1 —
+    the flag is all-reduced on the device and its copy is awaited one step later."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    s_bad = 4  # after the RCCL-statistics tuning steps
+    mp.spawn(_guard_worker, args=(2, port, str(tmp_path), s_bad), nprocs=2, join=True)
+    for r in range(2):
+        at = int((tmp_path / f"g{r}").read_text())
+        assert s_bad <= at <= s_bad + 1, (r, at)
+
+
 def test_site_table_exhaustion():
     t = SiteTable(8, region_words(8, 2, 64), 16)
     t.get("x", 2, 64)

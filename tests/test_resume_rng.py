@@ -27,7 +27,46 @@ def test_resume_restores_rng(tmp_path):
     assert np.array_equal(np.random.rand(4), want_n)
 
 
-@pytest.mark.parametrize("knob", ["SIMCLR_SKIP_WGRAD", "SIMCLR_EXPERIMENT_SKIP_BNRED"])
+def _rank_rng_worker(rank, world, port, path):
+    import os
+    import torch.distributed as dist
+    from simclr_amd.utils.checkpoint import gather_rng_states, restore_rng
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(100 + rank)  # every rank's generators differ
+    np.random.seed(100 + rank)
+    if rank == 0:
+        save_resume(path, ContrastiveModel("resnet18"), None, epoch=1, step=3,
+                    group=dist.group.WORLD)
+    else:
+        gather_rng_states(0, dist.group.WORLD)
+    want_t, want_n = torch.rand(4), np.random.rand(4)
+    dist.barrier()
+    torch.manual_seed(7)
+    np.random.seed(7)
+    restore_rng(torch.load(path, weights_only=True))
+    ok = torch.equal(torch.rand(4), want_t) and np.array_equal(np.random.rand(4), want_n)
+    with open(f"{path}.{rank}", "w") as f:
+        f.write("ok" if ok else "mismatch")
+    dist.destroy_process_group()
+
+
+def test_resume_restores_each_ranks_own_rng(tmp_path):
+    """Rank 0 writes the resume file, but every rank gets ITS OWN generators back (gathered at
+    save time, indexed by rank), not rank 0's copy."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    path = str(tmp_path / "resume-1.pt")
+    mp.spawn(_rank_rng_worker, args=(2, port, path), nprocs=2, join=True)
+    assert [open(f"{path}.{r}").read() for r in range(2)] == ["ok", "ok"]
+
+
+@pytest.mark.parametrize("knob",["SIMCLR_SKIP_WGRAD", "SIMCLR_EXPERIMENT_SKIP_BNRED"])
 def test_training_refuses_attribution_knobs(monkeypatch, knob):
     from simclr_amd.train.pretrain import pretrain
     from simclr_amd.train.supervised import supervised
