@@ -97,90 +97,6 @@ ConvFusion fusion_from(const c10::optional<Tensor>& pro_sc, const c10::optional<
 
 unsigned* tickets_for(const Tensor& like, int64_t n, int64_t slot);
 
-const float* tail_ptr(const std::vector<c10::optional<Tensor>>& t, size_t i, int64_t n,
-                      const char* name) {
-  if (i >= t.size() || !t[i].has_value() || !t[i]->defined()) return nullptr;
-  check_dev(*t[i], at::kFloat, name);
-  TORCH_CHECK(t[i]->numel() >= n, "igemm tail: ", name, " too small");
-  return t[i]->data_ptr<float>();
-}
-
-// BatchNorm finalize in the conv's last blocks (bn_tail.h).  tail_t = [mi, ss, rm, rv, nbt,
-// gamma, beta, dgamma, dbeta, coef, ipc_peers, ipc_arena, ipc_epoch, ipc_err], tail_f = [count,
-// eps, momentum], tail_i = [ipc_site, world, rank, ticket_slot].
-void set_tail(ConvFusion& f, const ConvGeom& g, int64_t M, int bm, int bn, const Tensor& stats,
-              int64_t stats_seg_blocks, int64_t epi_mode, const c10::optional<Tensor>& stats2,
-              int64_t mode, const std::vector<c10::optional<Tensor>>& t,
-              const std::vector<double>& tf, const std::vector<int64_t>& ti) {
-#ifndef SIMCLR_BN_TAIL
-  TORCH_CHECK(false, "igemm tail: this build has no conv-tail BatchNorm finalize (rebuild with "
-                     "SIMCLR_BUILD_BN_TAIL=1)");
-#endif
-  TORCH_CHECK(mode == 1 || mode == 2, "igemm tail: mode 1 (forward) or 2 (backward)");
-  TORCH_CHECK(stats.defined() && stats.numel() > 0 && f.seg_rows > 0 && stats_seg_blocks == 0,
-              "igemm tail: needs the stats partials of one launch with seg_rows");
-  TORCH_CHECK(!(stats2.has_value() && stats2->defined()), "igemm tail: no second BN stream");
-  TORCH_CHECK((mode == 1 && epi_mode == 0) || (mode == 2 && (epi_mode == 3 || epi_mode == 4)),
-              "igemm tail: forward finalize after epilogue 0, backward after 3 / 4");
-  const int S = (int)(M / f.seg_rows);
-  TORCH_CHECK(S >= 1 && S <= 2 && g.N % 64 == 0 && f.seg_rows % bm == 0,
-              "igemm tail: <= 2 segments, channels % 64 == 0");
-  TORCH_CHECK(tf.size() == 3 && ti.size() == 4, "igemm tail: scalar lists");
-  const int64_t C = g.N, SC = (int64_t)S * C;
-  BnTailArgs& a = f.tail;
-  a.on = (int)mode;
-  a.nmb_seg = f.seg_rows / bm;
-  igemm_tail_plan(a.nmb_seg, &a.gr, &a.ngrp);
-  const int nNb = (g.N + bn - 1) / bn;
-  TORCH_CHECK(igemm_tail_ticket_words(nNb, S, a.ngrp) <= 4096, "igemm tail: ticket array");
-  BnFin& fin = a.fin;
-  fin.mode = (int)mode; fin.S = S; fin.C = (int)C;
-  fin.count = (float)tf[0]; fin.eps = (float)tf[1]; fin.momentum = (float)tf[2];
-  fin.mi = const_cast<float*>(tail_ptr(t, 0, 2 * SC, "mi"));
-  TORCH_CHECK(fin.mi != nullptr, "igemm tail: mi required");
-  if (mode == 1) {
-    fin.ss = const_cast<float*>(tail_ptr(t, 1, 2 * SC, "ss"));
-    fin.rm = const_cast<float*>(tail_ptr(t, 2, C, "running_mean"));
-    fin.rv = const_cast<float*>(tail_ptr(t, 3, C, "running_var"));
-    if (t.size() > 4 && t[4].has_value() && t[4]->defined()) {
-      check_dev(*t[4], at::kLong, "num_batches_tracked");
-      fin.nbt = t[4]->data_ptr<int64_t>();
-    }
-    fin.beta = tail_ptr(t, 6, C, "beta");
-  } else {
-    fin.dgamma = const_cast<float*>(tail_ptr(t, 7, C, "dgamma"));
-    fin.dbeta = const_cast<float*>(tail_ptr(t, 8, C, "dbeta"));
-    fin.coef = const_cast<float*>(tail_ptr(t, 9, 3 * SC, "coef"));
-    TORCH_CHECK(fin.coef != nullptr, "igemm tail: coef required");
-  }
-  fin.gamma = tail_ptr(t, 5, C, "gamma");
-  if (ti[1] > 1) {
-    TORCH_CHECK(t.size() == 14 && t[10].has_value() && t[11].has_value() && t[12].has_value() &&
-                    t[13].has_value(), "igemm tail: IPC exchange tensors");
-    const int64_t world = ti[1], rank = ti[2];
-    TORCH_CHECK(world <= 16 && rank >= 0 && rank < world, "igemm tail: world / rank");
-    check_dev(*t[10], at::kLong, "ipc_peers");
-    check_dev(*t[11], at::kLong, "ipc_arena");
-    check_dev(*t[12], at::kInt, "ipc_epoch");
-    check_dev(*t[13], at::kInt, "ipc_err");
-    TORCH_CHECK(t[10]->numel() == world && t[12]->numel() >= C / 64, "igemm tail: IPC tables");
-    TORCH_CHECK(ti[0] >= 0 && ti[0] + bn_ipc_region_words((int)world, S, (int)C) <= t[11]->numel(),
-                "igemm tail: IPC site outside the arena");
-    fin.ipc.peers = reinterpret_cast<uint64_t* const*>(t[10]->data_ptr<int64_t>());
-    fin.ipc.own = reinterpret_cast<uint64_t*>(t[11]->data_ptr<int64_t>());
-    fin.ipc.site = ti[0];
-    fin.ipc.epoch = reinterpret_cast<unsigned*>(t[12]->data_ptr<int>());
-    fin.ipc.err = t[13]->data_ptr<int>();
-    fin.ipc.world = (int)world;
-    fin.ipc.rank = (int)rank;
-  }
-  TORCH_CHECK(ti[3] >= 0 && ti[3] < 2, "igemm tail: ticket slot");
-  a.tick = tickets_for(stats, 4096, 2 + ti[3]);
-  // level-2 rows: only this launch uses them, on the current stream, so returning the block to
-  // the caching allocator right after the launch is safe (later users are stream-ordered)
-  at::Tensor ws = at::empty({(int64_t)S * a.ngrp * 2 * C}, stats.options().dtype(at::kFloat));
-  a.ws = ws.data_ptr<float>();
-}
 
 void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optional<Tensor>& bias,
            const c10::optional<Tensor>& stats, std::vector<int64_t> gv,
@@ -194,9 +110,7 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const c10::optional<Tensor>& epi_mi2, const c10::optional<Tensor>& stats2,
            const c10::optional<Tensor>& pro_d, const c10::optional<Tensor>& A2,
            const c10::optional<Tensor>& pro_rss, const c10::optional<Tensor>& pro_out,
-           const c10::optional<Tensor>& pro_mask, int64_t tail_mode,
-           const std::vector<c10::optional<Tensor>>& tail_t, std::vector<double> tail_f,
-           std::vector<int64_t> tail_i, int64_t stats_groups) {
+           const c10::optional<Tensor>& pro_mask) {
   const ConvGeom g = geom_from(gv);
   // bit 8 of epi_mode: epi_a is the stride-2 subsampled residual (conv.hip epi_load_batch)
   const bool epi_sub = (epi_mode & 256) != 0;
@@ -224,7 +138,7 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   }
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.N, "igemm: bias size");
   const bool has_stats = stats.has_value() && stats->defined();
-  if (has_stats && stats_seg_blocks == 0 && stats_groups == 0)
+  if (has_stats && stats_seg_blocks == 0)
     TORCH_CHECK(stats->numel() >= ((M + bm - 1) / bm) * 2 * g.N, "igemm: stats buffer too small");
   const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
                       g.OWp == g.OW;
@@ -252,12 +166,13 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
     const int64_t nseg = M / seg_rows;
     TORCH_CHECK(stats_base >= 0 && stats_base + seg_rows / bm <= stats_seg_blocks,
                 "igemm: stats remap window out of range");
-    TORCH_CHECK(stats_groups > 0 || stats->numel() >= nseg * stats_seg_blocks * 2 * g.N,
+    TORCH_CHECK(stats->numel() >= nseg * stats_seg_blocks * 2 * g.N,
                 "igemm: remapped stats buffer too small");
   }
   if (epi_mode == 3 || epi_mode == 4) {
     TORCH_CHECK(seg_rows > 0, "igemm mode 3/4 needs seg_rows");
-    TORCH_CHECK(!f.pro_sc || epi_mode == 3, "igemm: no prologue with epilogue mode 4");
+    TORCH_CHECK(!f.pro_sc || epi_mode == 3 || (pro_d.has_value() && pro_d->defined()),
+                "igemm: the BN-apply prologue takes epilogue mode 3 only (mode 4: BN-backward)");
     const int64_t nseg = M / seg_rows;
     f.epi_mi = optf32(epi_mi, "epi_mi");
     f.epi_S = (int)nseg;
@@ -294,7 +209,8 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
     TORCH_CHECK(f.pro_sc, "igemm BN-backward prologue needs pro_sc (A) and pro_sh (B)");
     TORCH_CHECK(pro_d->numel() >= (M / pro_seg_rows) * g.C, "igemm prologue: d [S][C] size");
     TORCH_CHECK(A2.has_value() && A2->numel() == A.numel(), "igemm prologue: A2 must match A");
-    TORCH_CHECK(epi_mode == 0 || epi_mode == 3, "igemm BN-backward prologue: epilogue 0 or 3");
+    TORCH_CHECK(epi_mode == 0 || epi_mode == 3 || epi_mode == 4,
+                "igemm BN-backward prologue: epilogue 0, 3 or 4");
     f.pro_d = f32(*pro_d, "pro_d");
     f.A2 = bf(*A2, "A2");
   }
@@ -330,60 +246,8 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
       f.pro_rsh = f.pro_rsc + nseg * g.C;
     }
   }
-  if (stats_groups > 0) {
-    TORCH_CHECK(has_stats && seg_rows > 0 && tail_mode == 0 && stats_groups <= 64,
-                "igemm: atomic stats replicas need stats, seg_rows, no tail, <= 64 groups");
-    TORCH_CHECK(stats->numel() >= (M / seg_rows) * stats_groups * 2 * g.N,
-                "igemm: atomic stats buffer too small ([S][G][2][N])");
-    if (stats2.has_value() && stats2->defined())
-      TORCH_CHECK(stats2->numel() >= stats->numel(), "igemm: stats2 buffer too small");
-    f.stats_groups = (int)stats_groups;
-  }
-  if (tail_mode != 0) set_tail(f, g, M, bm, igemm_variant_bn((int)variant), has_stats ? *stats : out, stats_seg_blocks, epi_mode,
-                               stats2, tail_mode, tail_t, tail_f, tail_i);
   conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
                 optf32w(stats, "stats"), f, (int)variant, cur_stream());
-}
-
-void igemm_plain(const Tensor& A, const Tensor& B, const Tensor& out,
-                 const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
-                 std::vector<int64_t> gv, const c10::optional<Tensor>& pro_sc,
-                 const c10::optional<Tensor>& pro_sh, int64_t pro_seg_rows, bool pro_relu,
-                 int64_t epi_mode, const c10::optional<Tensor>& epi_a,
-                 const c10::optional<Tensor>& epi_b, int64_t variant,
-                 const c10::optional<Tensor>& epi_ss, const c10::optional<Tensor>& epi_mi,
-                 int64_t seg_rows, int64_t stats_seg_blocks, int64_t stats_base,
-                 const c10::optional<Tensor>& epi_c, const c10::optional<Tensor>& epi_mask,
-                 const c10::optional<Tensor>& epi_c2, const c10::optional<Tensor>& epi_mi2,
-                 const c10::optional<Tensor>& stats2, const c10::optional<Tensor>& pro_d,
-                 const c10::optional<Tensor>& A2, const c10::optional<Tensor>& pro_rss,
-                 const c10::optional<Tensor>& pro_out, const c10::optional<Tensor>& pro_mask,
-                 int64_t stats_groups) {
-  igemm(A, B, out, bias, stats, std::move(gv), pro_sc, pro_sh, pro_seg_rows, pro_relu, epi_mode,
-        epi_a, epi_b, variant, epi_ss, epi_mi, seg_rows, stats_seg_blocks, stats_base, epi_c,
-        epi_mask, epi_c2, epi_mi2, stats2, pro_d, A2, pro_rss, pro_out, pro_mask, 0, {}, {}, {},
-        stats_groups);
-}
-
-void igemm_tailed(const Tensor& A, const Tensor& B, const Tensor& out,
-                  const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
-                  std::vector<int64_t> gv, const c10::optional<Tensor>& pro_sc,
-                  const c10::optional<Tensor>& pro_sh, int64_t pro_seg_rows, bool pro_relu,
-                  int64_t epi_mode, const c10::optional<Tensor>& epi_a,
-                  const c10::optional<Tensor>& epi_b, int64_t variant,
-                  const c10::optional<Tensor>& epi_ss, const c10::optional<Tensor>& epi_mi,
-                  int64_t seg_rows, int64_t stats_seg_blocks, int64_t stats_base,
-                  const c10::optional<Tensor>& epi_c, const c10::optional<Tensor>& epi_mask,
-                  const c10::optional<Tensor>& epi_c2, const c10::optional<Tensor>& epi_mi2,
-                  const c10::optional<Tensor>& stats2, const c10::optional<Tensor>& pro_d,
-                  const c10::optional<Tensor>& A2, const c10::optional<Tensor>& pro_rss,
-                  const c10::optional<Tensor>& pro_out, const c10::optional<Tensor>& pro_mask,
-                  int64_t tail_mode, const std::vector<c10::optional<Tensor>>& tail_t,
-                  std::vector<double> tail_f, std::vector<int64_t> tail_i) {
-  igemm(A, B, out, bias, stats, std::move(gv), pro_sc, pro_sh, pro_seg_rows, pro_relu, epi_mode,
-        epi_a, epi_b, variant, epi_ss, epi_mi, seg_rows, stats_seg_blocks, stats_base, epi_c,
-        epi_mask, epi_c2, epi_mi2, stats2, pro_d, A2, pro_rss, pro_out, pro_mask, tail_mode,
-        tail_t, std::move(tail_f), std::move(tail_i), 0);
 }
 
 int64_t igemm_bm(int64_t N) { return igemm_block_m((int)N); }
@@ -417,7 +281,7 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
            const c10::optional<Tensor>& pro_sc, const c10::optional<Tensor>& pro_sh,
            int64_t pro_seg_rows, bool pro_relu, int64_t pro_S, int64_t variant,
            const c10::optional<Tensor>& dY2, const c10::optional<Tensor>& dp_coef,
-           int64_t dp_seg_rows, int64_t dp_S, const c10::optional<Tensor>& tickets) {
+           int64_t dp_seg_rows, int64_t dp_S) {
   const ConvGeom g = geom_from(gv);
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int64_t K = (int64_t)g.KH * g.KW * g.C;
@@ -451,15 +315,8 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
     f.dp_seg_rows = (int)dp_seg_rows;
     f.dp_S = (int)dp_S;
   }
-  int* tk = nullptr;
-  if (tickets.has_value() && tickets->defined()) {
-    check_dev(*tickets, at::kInt, "tickets");
-    TORCH_CHECK(tickets->numel() >= wgrad_tiles(g, (int)variant),
-                "wgrad: tickets must hold one word per output tile");
-    tk = tickets->data_ptr<int>();
-  }
   conv_wgrad(g, bf(dY, "dY"), bf(X, "X"), (size_t)X.numel(), f32w(partial, "partial"), (int)splits,
-             f32w(out, "out"), (int)creal, (float)beta, f, (int)variant, cur_stream(), tk);
+             f32w(out, "out"), (int)creal, (float)beta, f, (int)variant, cur_stream());
 }
 
 
@@ -642,11 +499,8 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
                         const c10::optional<Tensor>& ipc_peers,
                         const c10::optional<Tensor>& ipc_arena, int64_t ipc_site,
                         const c10::optional<Tensor>& ipc_epoch,
-                        const c10::optional<Tensor>& ipc_err, int64_t world, int64_t rank,
-                        bool zero_after) {
+                        const c10::optional<Tensor>& ipc_err, int64_t world, int64_t rank) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "bn_reduce_fused: mode");
-  TORCH_CHECK(!zero_after || nblk <= bn_reduce_direct_rows(),
-              "bn_reduce_fused: zero_after needs the one-pass (direct) reduction");
   TORCH_CHECK(nblk > 0 && partial.numel() >= S * nblk * 2 * C, "bn_reduce_fused: partial size");
   TORCH_CHECK(C % 4 == 0, "bn_reduce_fused: C must be a multiple of 4 (float4 partial rows)");
   TORCH_CHECK(S >= 1 && S <= 4, "bn_reduce_fused: at most 4 segments");
@@ -657,7 +511,6 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
   at::Tensor ws = at::empty({S * G * 2 * C}, partial.options());
   q.ws = ws.data_ptr<float>();
   q.tickets = tickets_for(partial, (C + 63) / 64, ticket_slot);
-  q.zero_after = zero_after ? 1 : 0;
   q.count = (float)count; q.eps = (float)eps; q.momentum = (float)momentum;
   if (mode == 0) {
     TORCH_CHECK(stats.has_value() && stats->numel() >= 2 * S * C, "bn_reduce_fused: stats");
@@ -712,8 +565,6 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
     q.world = (int)world;
     q.rank = (int)rank;
   }
-  static const bool skip_for_timing = getenv("SIMCLR_EXPERIMENT_SKIP_BNRED") != nullptr;
-  if (skip_for_timing) return;  // timing experiment only: statistics left stale
   bn_reduce_fused(q, cur_stream());
 }
 
@@ -1035,8 +886,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
   m.def("ce_topk(Tensor logits, Tensor y, float gscale, Tensor(a!) loss, Tensor(b!) rank, Tensor(c!)? dlogits=None) -> ()", &ce_topk_op);
   m.def("class_sums(Tensor X, Tensor y, int NC, Tensor(a!) sums, Tensor(b!) counts) -> ()", &class_sums_op);
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None, int stats_groups=0) -> ()", &igemm_plain);
-  m.def("igemm_t(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc, Tensor? pro_sh, int pro_seg_rows, bool pro_relu, int epi_mode, Tensor? epi_a, Tensor? epi_b, int variant, Tensor? epi_ss, Tensor? epi_mi, int seg_rows, int stats_seg_blocks, int stats_base, Tensor? epi_c, Tensor? epi_mask, Tensor? epi_c2, Tensor? epi_mi2, Tensor(c!)? stats2, Tensor? pro_d, Tensor? A2, Tensor? pro_rss, Tensor(d!)? pro_out, Tensor(e!)? pro_mask, int tail_mode, Tensor(f!)?[] tail_t, float[] tail_f, int[] tail_i) -> ()", &igemm_tailed);
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm);
   m.def("igemm_dual_ok(int v, int[] geom) -> bool", &igemm_dok);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
@@ -1052,7 +902,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("wgrad_tiles(int[] geom, int variant=-1) -> int", &wgrad_ntiles);
   m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor xss, Tensor xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps) -> ()", &conv1x1_bwd_dual_op);
   m.def("wgrad_reduce_slabs(Tensor(a!) partial, int splits, Tensor(b!) out, float beta=0.0) -> ()", &wgrad_reduce_slabs_op);
-  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1, Tensor(c!)? tickets=None) -> ()", &wgrad);
+  m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);
   m.def("weight_transform_plan(Tensor[] Ws, Tensor[] Wts, int[] p) -> Tensor", &weight_transform_plan);
   m.def("weight_transform_batch(Tensor table, int total_blocks) -> ()", &weight_transform_batch);
@@ -1060,7 +910,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
   m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
-  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0, bool zero_after=False) -> ()", &bn_reduce_fused_op);
+  m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0) -> ()", &bn_reduce_fused_op);
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);

@@ -178,7 +178,6 @@ struct BnReduceArgs {
   unsigned* epoch;
   int* err;
   int world, rank;
-  int zero_after;
 };
 
 constexpr int kMaxSeg = 4;  // BatchNorm segments (views) per launch handled by the reducer
@@ -349,9 +348,6 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
             float4* src = (float4*)(base + (((size_t)sg * G + g) * 2) * C);
             const float4 v = *src;
             acc[sg].x += v.x; acc[sg].y += v.y; acc[sg].z += v.z; acc[sg].w += v.w;
-            // atomic accumulators (conv stats_groups) are ready for the next step once read:
-            // each element has exactly one reader (direct mode)
-            if (p.zero_after) *src = make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
       }
@@ -927,23 +923,13 @@ void bn_stats_partial(const uint16_t* x, int R, int C, int S, float* partial, in
   HIP_CHECK_LAUNCH();
 }
 
-int bn_reduce_direct_rows() {
-  static int d = -1;
-  if (d < 0) {
-    const char* e = getenv("SIMCLR_BNRED_DIRECT");
-    d = e ? atoi(e) : 64;  // measured: direct wins only for the smallest partials
-  }
-  return d;
-}
+// measured: the one-pass (direct) reduce wins only for the smallest partials
+int bn_reduce_direct_rows() { return 64; }
 
 int bn_reduce_groups(int nblk) {
-  static int rows = -1, cap = -1;  // tuning overrides (tools/bench_reduce.py)
-  if (rows < 0) {
-    const char* e = getenv("SIMCLR_BNRED_ROWS");
-    const char* f = getenv("SIMCLR_BNRED_CAP");
-    rows = e ? atoi(e) : 128;  // measured (tools/bench_reduce.py): few slices beat many — the
-    cap = f ? atoi(f) : 16;    // per-group ticket atomics serialise and the consumer reads all
-  }
+  // measured (tools/bench_reduce.py, r2): few slices beat many — the per-group ticket
+  // atomics serialise and the consumer reads all
+  constexpr int rows = 128, cap = 16;
   if (nblk <= rows) return 1;
   int g = (nblk + rows - 1) / rows;  // ~rows partial rows per level-1 block
   return g > cap ? cap : g;
@@ -986,7 +972,6 @@ void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s) {
   a.dgamma = q.dgamma; a.dbeta = q.dbeta; a.coef = q.coef;
   a.peers = q.ipc_peers; a.own = q.ipc_own; a.site = q.ipc_site; a.epoch = q.ipc_epoch;
   a.err = q.ipc_err; a.world = q.world; a.rank = q.rank;
-  a.zero_after = q.zero_after;
   const dim3 grid = a.direct ? dim3((q.C + 63) / 64) : dim3((q.C + 63) / 64, q.S, a.G);
   if (a.world > 1 && a.peers != nullptr)
     hipLaunchKernelGGL(k_bn_reduce_fused<true>, grid, dim3(256), 0, s, a);

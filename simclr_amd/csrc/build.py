@@ -60,8 +60,6 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
     BUILD.mkdir(exist_ok=True)
     opt = ["-O0", "-g"] if debug else ["-O3"]
     common = [f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", *opt, "-Wno-unused-result"]
-    if os.environ.get("SIMCLR_BUILD_BN_TAIL") == "1":  # BatchNorm finalize in conv tails (opt-in)
-        common.append("-DSIMCLR_BN_TAIL")
     headers = [HERE / h for h in HEADERS]
     tasks = []
     objs = []

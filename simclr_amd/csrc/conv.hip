@@ -26,7 +26,6 @@
 // with an XOR chunk swizzle (cdna_hip_programming.md T2), XCD-aware block remap (T1).
 #include "common.h"
 #include "kernels.h"
-#include "bn_tail.h"
 
 #include <type_traits>
 
@@ -83,12 +82,6 @@ struct IgemmArgs {
   // stats row remap (segment-major partials when one BN's rows span several launches):
   //   blk = seg * stats_seg_blocks + stats_base + (m0 - seg * seg_rows) / BM, seg = m0 / seg_rows
   int seg_rows, stats_seg_blocks, stats_base;
-  // BatchNorm finalize in this launch's last blocks (igemm_bn_tail; on == 0: partials only)
-  BnTailArgs tail;
-  // > 0: the partials are accumulated with float atomics into stats_groups replica rows per
-  // segment ([S][G][2][N], zeroed by the reduce that consumes them) instead of one row per
-  // row-block: the reduce reads S·G rows in one pass (bn.hip direct mode)
-  int stats_groups;
 };
 
 __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const float* sh, bool ok,
@@ -225,105 +218,6 @@ __device__ __forceinline__ void epi_load_batch(const IgemmArgs& p, int m0, int n
 template <int EPI>
 constexpr bool epi_prefetch() { return EPI == 3 || EPI == 4 || EPI == 5; }
 
-// BatchNorm finalize in the last blocks of the launch (bn_tail.h): the last of every level-1
-// group of `gr` row-blocks (same segment, same channel tile) sums the group's partial rows; the
-// last of those per channel tile sums the groups of every segment, runs the cross-rank exchange
-// (world > 1) and finalizes the tile's channels.  Fixed summation order: deterministic.
-template <int BM, int BN, int NT>
-__device__ void igemm_bn_tail(const IgemmArgs& p, int m0, int n0, int mb, char* smem) {
-  const BnTailArgs& t = p.tail;
-  const int S = t.fin.S, N = p.N, tid = threadIdx.x;
-  const int nb = n0 / BN;
-  const int seg = m0 / p.seg_rows;
-  const int local = mb - seg * t.nmb_seg;
-  const int grp = local / t.gr;
-  const int gbeg = grp * t.gr, gend = min(t.nmb_seg, gbeg + t.gr);
-  int* flag = (int*)smem;
-  unsigned* sh_ep = (unsigned*)smem + 4;
-  float* v = (float*)smem + 16;  // [S][2][BN]
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partial row has landed
-  __syncthreads();
-  if (tid == 0) {
-    unsigned* tk = t.tick + ((size_t)nb * S + seg) * t.ngrp + grp;
-    const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (unsigned)(gend - gbeg - 1);
-    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  // level 1: the group's rows of this channel tile
-  for (int q = tid; q < 2 * BN; q += NT) {
-    const int k = q / BN, j = q - k * BN, n = n0 + j;
-    if (n >= N) continue;
-    const float* src = p.stats + ((size_t)(seg * t.nmb_seg) * 2 + k) * N + n;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int r = gbeg;
-    for (; r + 3 < gend; r += 4) {
-      a0 += src[(size_t)r * 2 * N];
-      a1 += src[(size_t)(r + 1) * 2 * N];
-      a2 += src[(size_t)(r + 2) * 2 * N];
-      a3 += src[(size_t)(r + 3) * 2 * N];
-    }
-    for (; r < gend; ++r) a0 += src[(size_t)r * 2 * N];
-    __hip_atomic_store(&t.ws[(((size_t)seg * t.ngrp + grp) * 2 + k) * N + n], (a0 + a1) + (a2 + a3),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    unsigned* tk = t.tick + (size_t)p.nNb * S * t.ngrp + nb;
-    const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (unsigned)(S * t.ngrp - 1);
-    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  // level 2: every segment's group sums of this channel tile, in group order
-  for (int q = tid; q < S * 2 * BN; q += NT) {
-    const int sk = q / BN, j = q - sk * BN, n = n0 + j;
-    float a = 0.f;
-    if (n < N)
-      for (int g = 0; g < t.ngrp; ++g)
-        a += t.ws[(((size_t)(sk >> 1) * t.ngrp + g) * 2 + (sk & 1)) * N + n];
-    v[q] = a;
-  }
-  __syncthreads();
-  float l1[kTailMaxS], l2[kTailMaxS];  // rank-local sums (dγ, dβ)
-  if (tid < BN) {
-#pragma unroll
-    for (int sg = 0; sg < kTailMaxS; ++sg) {
-      l1[sg] = sg < S ? v[(sg * 2) * BN + tid] : 0.f;
-      l2[sg] = sg < S ? v[(sg * 2 + 1) * BN + tid] : 0.f;
-    }
-  }
-  if (t.fin.ipc.peers != nullptr && t.fin.ipc.world > 1)
-    tail_ipc_exchange(t.fin.ipc, S, N, n0, BN, v, sh_ep);
-  if (tid < BN && n0 + tid < N) {
-    float g1[kTailMaxS], g2[kTailMaxS];
-#pragma unroll
-    for (int sg = 0; sg < kTailMaxS; ++sg) {
-      g1[sg] = sg < S ? v[(sg * 2) * BN + tid] : 0.f;
-      g2[sg] = sg < S ? v[(sg * 2 + 1) * BN + tid] : 0.f;
-    }
-    bn_fin_col(t.fin, n0 + tid, g1, g2, l1, l2);
-  }
-  if (t.fin.mode == 1 && nb == 0 && tid == 0 && t.fin.nbt != nullptr) t.fin.nbt[0] += S;
-}
-
-// Epilogue shared by the igemm kernels: bias, bf16 round, LDS-staged 16-B row stores, fused
-// elementwise modes 1-5 and the per-block BatchNorm partial statistics (see IgemmArgs).
 template <int BM, int BN, int WM, int WN, int NT, int EPI>
 __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
                                                f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
@@ -505,39 +399,13 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
       const int blk = p.stats_seg_blocks > 0
                           ? seg * p.stats_seg_blocks + p.stats_base + (m0 - seg * p.seg_rows) / BM
                           : mb;
-      if (p.stats_groups > 0) {
-        // replica g of this row-block's segment: 2048 row-blocks of a layer1 conv become
-        // 16 rows with ~128 uncontended adds per address, spread over L2 channels
-        const int segb = (p.stats_seg_blocks > 0 ? p.stats_base : 0) + (m0 - seg * p.seg_rows) / BM;
-        const size_t row = (size_t)seg * p.stats_groups + (segb % p.stats_groups);
-        unsafeAtomicAdd(&p.stats[(row * 2 + 0) * p.N + n0 + tid], a);
-        unsafeAtomicAdd(&p.stats[(row * 2 + 1) * p.N + n0 + tid], b);
-        if (two) {
-          unsafeAtomicAdd(&p.stats2[(row * 2 + 0) * p.N + n0 + tid], a);
-          unsafeAtomicAdd(&p.stats2[(row * 2 + 1) * p.N + n0 + tid], d);
-        }
-      } else if (p.tail.on) {
-        // write-through (agent-scope) stores: this kernel's tail may read them from another
-        // XCD (bn_tail.h); a separate reduce kernel sees plain stores at the kernel boundary
-        __hip_atomic_store(&p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid], a, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid], b, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
-        p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
-      }
-      if (two && p.stats_groups == 0) {
+      p.stats[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
+      p.stats[((size_t)blk * 2 + 1) * p.N + n0 + tid] = b;
+      if (two) {
         p.stats2[((size_t)blk * 2 + 0) * p.N + n0 + tid] = a;
         p.stats2[((size_t)blk * 2 + 1) * p.N + n0 + tid] = d;
       }
     }
-#ifdef SIMCLR_BN_TAIL  // opt-in build (SIMCLR_BUILD_BN_TAIL=1): the compiled-in tail alone
-                       // costs 0.18 ms/step even when off at run time (A/B, r2 log)
-    if (EPI == 0 || EPI == 3 || EPI == 4) {
-      if (p.tail.on) igemm_bn_tail<BM, BN, NT>(p, m0, n0, mb, smem);
-    }
-#endif
   }
 }
 
@@ -1255,181 +1123,6 @@ constexpr int PP_NINSTR = 43;                  // patch DMA instructions (8 pixe
 constexpr int PP_PSZ = PP_NINSTR * 512;        // patch buffer, elements
 constexpr int PP_LDS = 9 * 64 * 64 * 2 + 2 * PP_PSZ * 2 + 1024;
 
-template <int EPI, int PRO>
-__global__ __launch_bounds__(512, 1) void igemm_ppatch(IgemmArgs p) {
-  constexpr int BM = 256, BN = 64, WM = 8, WN = 1, NW = 8, NT = 512;
-  constexpr int TM = BM / WM, FM = TM / 16, FN = BN / 16;  // 2 x 4 fragments per wave
-  constexpr int C = 64, OW = 32, PW = 34, PP = 340, NK = 9;
-  constexpr uint32_t PBYTES = PP_PSZ * 2;  // one patch buffer (44,032 B)
-  constexpr uint32_t WOFF = 2 * PBYTES;    // weights behind the two patches
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* Pb = (uint16_t*)smem;                // [2][PP_PSZ] patch images
-  uint16_t* Ws = (uint16_t*)(smem + WOFF);       // [9][64 rows][64], chunk-swizzled (igemm_patch Bs)
-  float* Tb = (float*)(smem + WOFF + NK * BN * 64 * 2);  // PRO: [segment 0, 1][sc, sh][64]
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntiles = p.M / BM;
-  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
-  const int t_beg = lbid * per;
-  const int t_end = min(ntiles, t_beg + per);
-  if (t_beg >= t_end) return;  // block-uniform: no barrier is skipped by part of a block
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
-
-  if (PRO) {  // both segments' tables, before any DMA (a global load consumed later would drain it)
-    for (int i = tid; i < 2 * 2 * C; i += NT) {
-      const int sg = i / (2 * C), k = (i / C) & 1, c = i % C;
-      const int sgc = sg * p.pro_seg_rows < p.M ? sg : 0;
-      Tb[i] = (k ? p.pro_sh : p.pro_sc)[sgc * C + c];
-    }
-  }
-  // resident weights: k-step kt = rows (co) x 64 (tap kt's channels); lane → (row, chunk)
-  {
-    const int lrow = lane >> 3, lbch = (lane & 7) ^ (lane >> 3);
-    const uint32_t off = (uint32_t)((wid * 8 + lrow) * p.K + lbch * 8) * 2u;
-#pragma unroll
-    for (int kt = 0; kt < NK; ++kt)
-      dma16_opaque(rb, Ws + kt * BN * 64 + wid * 8 * 64, off + (uint32_t)(kt * 64) * 2u);
-  }
-  auto issue_patch = [&](int t, uint16_t* P) {
-    const int m0 = t * BM;
-    const int img = m0 / (p.OH * OW);
-    const int row0 = (m0 - img * p.OH * OW) / OW;
-    for (int i = wid; i < PP_NINSTR; i += NW) {
-      const int q = i * 8 + (lane >> 3);
-      const int pch = lane & 7;
-      const int lch = pch ^ (q & 7);
-      const int pr = q / PW, pc = q - (q / PW) * PW;
-      const int ih = row0 - 1 + pr, iw = pc - 1;
-      const bool ok = q < PP && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-      const uint32_t off =
-          ok ? (uint32_t)((((img * p.IH + ih) * p.IW + iw) * C + lch * 8) * 2) : p.a_bytes;
-      dma16_opaque(ra, P + i * 512, off);
-    }
-  };
-  issue_patch(t_beg, Pb);
-
-  // Fragment addresses, fixed for every tile: the A fragment of (tap, k-half, fm) is pixel
-  // q = (frow + kh)·PW + fcol + kw at XOR-swizzled chunk (ks·4 + lane/16) ^ (q & 7) — the swizzle
-  // keys on the shifted pixel, so the addresses are not affine in the tap: all 36 are computed
-  // once (VGPR byte offsets into patch buffer 0; buffer 1 is a +44,032 immediate, the tile loop
-  // being unrolled by 2) instead of ~30 VALU of index math per k-half per tile.  The B fragments
-  // of every tap share one row/chunk pattern (the tap is a +8 KiB immediate).
-  uint32_t aoff[NK][2][FM];
-  uint32_t boff[2][FN];
-#pragma unroll
-  for (int fm = 0; fm < FM; ++fm) {
-    const int m = wid * TM + fm * 16 + (lane & 15);
-    const int qb = (m / OW) * PW + (m % OW);
-#pragma unroll
-    for (int kt = 0; kt < NK; ++kt)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int q = qb + (kt / 3) * PW + (kt % 3);
-        const int ch = (ks * 4 + (lane >> 4)) ^ (q & 7);
-        aoff[kt][ks][fm] = (uint32_t)(q * C + ch * 8) * 2u;
-      }
-  }
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int row = fn * 16 + (lane & 15);
-      const int ch = (ks * 4 + (lane >> 4)) ^ (row & 7);
-      boff[ks][fn] = WOFF + (uint32_t)(row * 64 + ch * 8) * 2u;
-    }
-
-  auto tile = [&](int t, auto curc) {
-    constexpr int cur = decltype(curc)::value;
-    const char* P = smem + cur * PBYTES;
-    const int m0 = t * BM;
-    // this tile's patch (issued a tile ago; the weights too on the first tile) has landed; the
-    // previous tile's 4 output stores per thread, issued after it, may stay in flight
-    if (t == t_beg)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // patch visible to every wave; the other buffer is free
-    if (t + 1 < t_end) issue_patch(t + 1, Pb + (cur ^ 1) * PP_PSZ);
-    if (PRO) {
-      // BN-apply + ReLU on the landed patch (see igemm_patch): chunks 64 pixels apart share
-      // their logical channel chunk; out-of-image pixels stay zero
-      const int pseg = m0 / p.pro_seg_rows;
-      const int img = m0 / (p.OH * OW);
-      const int row0 = (m0 - img * p.OH * OW) / OW;
-      const int q0 = tid >> 3;
-      const int ch = ((tid & 7) ^ (q0 & 7)) * 8;
-      const float4* ps = (const float4*)(Tb + pseg * 2 * C + ch);
-      const float4* ph = (const float4*)(Tb + pseg * 2 * C + C + ch);
-      const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
-      const f32x2 sc[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
-      const f32x2 sh[4] = {{h0.x, h0.y}, {h0.z, h0.w}, {h1.x, h1.y}, {h1.z, h1.w}};
-      constexpr int DR = 64 / PW, DC = 64 - DR * PW;
-      int pr = q0 / PW, pc = q0 - (q0 / PW) * PW;
-      uint16_t* base = (uint16_t*)P + tid * 8;
-      const bool relu = p.pro_relu != 0;
-#pragma unroll
-      for (int i0 = 0; i0 < 8; i0 += 4) {
-        u32x4 v[4];
-        bool ok[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int ih = row0 - 1 + pr, iw = pc - 1;
-          ok[u] = (i0 + u) * 64 + q0 < PP && (unsigned)ih < (unsigned)p.IH &&
-                  (unsigned)iw < (unsigned)p.IW;
-          if (ok[u]) v[u] = *(const u32x4*)(base + (i0 + u) * NT * 8);
-          pr += DR;
-          pc += DC;
-          if (pc >= PW) { pc -= PW; ++pr; }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (ok[u]) *(u32x4*)(base + (i0 + u) * NT * 8) = affine_relu8_pk(v[u], sc, sh, relu);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    EpiBatch<epi_unr<BM, BN, NT>()> pre;
-    if (epi_prefetch<EPI>()) epi_load_batch<BM, BN, NT, EPI>(p, m0, 0, 0, pre);
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < NK; ++kt) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[FM], bfr[FN];
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-          af[fm] = *(const bf16x8*)(smem + cur * PBYTES + aoff[kt][ks][fm]);
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          bfr[fn] = *(const bf16x8*)(smem + kt * (BN * 64 * 2) + boff[ks][fn]);
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn)
-            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[fn], af[fm], acc[fm][fn], 0, 0, 0);
-      }
-    }
-    // every wave done reading this patch before the epilogue stages the C tile over it (raw
-    // barrier: the next patch's DMA stays in flight)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    igemm_epilogue<BM, BN, WM, WN, NT, EPI>(p, acc, (char*)P, m0, 0, t,
-                                            epi_prefetch<EPI>() ? &pre : nullptr);
-  };
-  for (int t = t_beg; t < t_end; t += 2) {
-    tile(t, std::integral_constant<int, 0>{});
-    if (t + 1 < t_end) tile(t + 1, std::integral_constant<int, 1>{});
-  }
-}
 
 // ------------------------------------------------------------------------------------ wgrad
 // Physical element offset of (row r, element col) in a W-wide swizzled LDS row (see wgrad_tn):
@@ -1459,17 +1152,11 @@ struct WgradArgs {
   const uint16_t* dY2;
   const float* dp_coef;
   int dp_seg_rows, dp_S;
-  // in-launch split reduction (wgrad_finish): per-tile arrival tickets (zeroed, self-resetting),
-  // the final [N][K] fp32 gradient and its accumulate factor; tickets == nullptr: the host
-  // launches the separate split-reduce kernels instead
-  int* tickets;
-  float* out;
-  float beta;
 };
 
 // One 64-deep step of the weight-gradient tile from swizzled row-major LDS images (rows = m):
 // both MFMA operands are read transposed with ds_read_b64_tr_b16.
-template <int BCO, int BKK, int WM, int WN>
+template <int BCO, int BKK, int WM, int WN, int KS = 2>
 __device__ __forceinline__ void wgrad_mma(const uint16_t* Db, const uint16_t* Xb,
                                           f32x4 (&acc)[BCO / WM / 16][BKK / WN / 16]) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
@@ -1480,7 +1167,7 @@ __device__ __forceinline__ void wgrad_mma(const uint16_t* Db, const uint16_t* Xb
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   typedef short i16x8 __attribute__((ext_vector_type(8)));
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
+  for (int ks = 0; ks < KS; ++ks) {
     const int r1 = ks * 32 + 8 * g + q;
     bf16x8 af[FM], bfr[FN];
 #pragma unroll
@@ -1533,56 +1220,6 @@ __device__ __forceinline__ float4 slab_sum4(const float4* __restrict__ p, size_t
                      (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
 }
 
-
-// In-launch split reduction (cdna_hip_programming.md §5 'In-launch split-K reduction'): every
-// block publishes its fp32 slab (plain stores → vmcnt(0) → barrier → agent-scope release) and
-// draws a ticket for its output tile; the block drawing splits−1 acquires and sums the tile's
-// slabs IN SPLIT ORDER (deterministic whichever block arrives last) straight into the gradient,
-// then resets the ticket for the next launch.  Replaces the separate wgrad_reduce_* launches
-// (79 per ResNet-50 step, ~16-22 µs each on the weight-gradient stream).  The tile's k columns
-// are NSEG runs of klen (one run for the tn / LDS-DMA tiles, one per tap for wgrad_patch);
-// LDS (the kernel's staging array, idle by now) carries the "last" flag.
-template <int NSEG>
-__device__ __forceinline__ void wgrad_finish(const WgradArgs& p, char* smem, int tile, int co0,
-                                             int nco, const int (&kbeg)[NSEG], int klen) {
-  if (p.tickets == nullptr) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  volatile int* flag = (volatile int*)smem;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(p.tickets + tile, 1, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == p.splits - 1;
-    if (last) {
-      __hip_atomic_store(p.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (*flag == 0) return;
-  const size_t slab4 = (size_t)p.N * p.K / 4;
-  const float4* part = (const float4*)p.partial;
-  float4* out = (float4*)p.out;
-  const int kq = klen >> 2;
-  const int per = nco * NSEG * kq;
-  for (int i = threadIdx.x; i < per; i += blockDim.x) {
-    const int kk = i % kq;
-    const int r = i / kq;
-    const int sg = r % NSEG;
-    const int co = co0 + r / NSEG;
-    const size_t e4 = (((size_t)co * p.K + kbeg[sg]) >> 2) + kk;
-    float4 v = slab_sum4(part + e4, slab4, p.splits);
-    if (p.beta != 0.f) {
-      const float4 o = out[e4];
-      v.x += p.beta * o.x; v.y += p.beta * o.y; v.z += p.beta * o.z; v.w += p.beta * o.w;
-    }
-    out[e4] = v;
-  }
-}
 
 // fp32 partial slab of one split: partial[split][co][k]
 template <int BCO, int BKK, int WM, int WN>
@@ -1801,8 +1438,6 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
     }
   }
   wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
-  const int kb[1] = {k0};
-  wgrad_finish<1>(p, smem, tile, co0, min(BCO, p.N - co0), kb, min(BKK, p.K - k0));
 }
 
 // Weight gradient with LDS-DMA staging (no operand prologue; C % 64 == 0): the dY and im2col(X)
@@ -1816,7 +1451,8 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 // counted vmcnt keeps step it+1's DMA in flight across the barrier (raw s_barrier: hipcc's
 // __syncthreads() would drain it with vmcnt(0)) — for the HBM-bound 1x1 weight gradients.
 template <int BCO, int BKK, int WM, int WN, bool PRO, int NST>
-__global__ __launch_bounds__(64 * WM * WN, NST == 1 ? 2 : 1) void wgrad_glds(WgradArgs p) {
+__global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
+  static_assert(NST == 2 || NST == 3, "wgrad_glds stages");
   constexpr int NW = WM * WN;
   constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = 64 / (RPD * NW);
   constexpr int CPX = BKK / 8, RPX = 64 / CPX, XI = 64 / (RPX * NW);
@@ -1945,7 +1581,7 @@ __global__ __launch_bounds__(64 * WM * WN, NST == 1 ? 2 : 1) void wgrad_glds(Wgr
   if (nit > 0) issue(0, 0);
   if (NST == 3 && nit > 1) issue(1, 1);
   for (int it = 0; it < nit; ++it) {
-    const int cur = NST == 3 ? it % 3 : NST == 2 ? (it & 1) : 0;
+    const int cur = NST == 3 ? it % 3 : (it & 1);
     if (NST == 3 && it + 1 < nit)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step it+1 stays in flight
     else
@@ -2006,19 +1642,147 @@ __global__ __launch_bounds__(64 * WM * WN, NST == 1 ? 2 : 1) void wgrad_glds(Wgr
       __builtin_amdgcn_s_barrier();
     }
     wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * BCO, Xs + cur * 64 * BKK, acc);
-    if constexpr (NST == 1) {
-      // single stage, 2 blocks per CU (the other block's MFMAs cover this one's DMA wait):
-      // every wave done reading the tile, then refill it
-      if (it + 1 < nit) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(it + 1, 0);
-      }
-    }
   }
   wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
-  const int kb[1] = {k0};
-  wgrad_finish<1>(p, smem, tile, co0, min(BCO, p.N - co0), kb, min(BKK, p.K - k0));
+}
+
+// Deep-pipelined LDS-DMA weight gradient (no operand prologues).  wgrad_glds stages 64-row
+// steps in two LDS buffers: the DMA of step it+1 is issued at the top of step it and must land
+// within ONE step of MFMAs (~0.4-0.9 us for the big tiles) — less than an HBM / remote-L2 round
+// trip under load, so every step waited on its data (MFMA busy ~23 %, r3 optimisation log).
+// Here a step is SR = 32 rows (one 16x16x32 MFMA k-step), the LDS holds NST steps and NST - 1 of
+// them are in flight: the DMA of step it + NST - 1 is issued right after the barrier of step it,
+// so it has NST - 1 steps of MFMAs to land.  A counted vmcnt keeps the later steps in flight
+// across the raw barrier (never vmcnt(0) in the loop: cdna_hip_programming.md "Pipelining
+// across barriers"); the barrier also publishes that every wave's fragment reads of the buffer
+// being refilled have retired (lgkmcnt(0) before it).  s_setprio(1) around the MFMA cluster
+// keeps hipcc from hoisting MFMAs across the barriers.
+template <int BCO, int BKK, int WM, int WN, int SR, int NST>
+__global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_pipe(WgradArgs p) {
+  constexpr int NW = WM * WN;
+  constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = SR / (RPD * NW);
+  constexpr int CPX = BKK / 8, RPX = 64 / CPX, XI = SR / (RPX * NW);
+  static_assert(SR % 32 == 0 && DI >= 1 && XI >= 1 && DI * RPD * NW == SR &&
+                    XI * RPX * NW == SR, "wgrad pipe mapping");
+  static_assert(NST >= 3 && NST <= 6, "wgrad pipe stages");
+  constexpr int PER = DI + XI;  // DMA instructions per wave per step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ds = (uint16_t*)smem;           // [NST][SR][BCO]
+  uint16_t* Xs = Ds + NST * SR * BCO;       // [NST][SR][BKK]
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = p.nCo * p.nKk;
+  const int split = lbid / tiles;
+  const int tile = lbid % tiles;
+  const int co0 = (tile / p.nKk) * BCO;
+  const int k0 = (tile % p.nKk) * BKK;
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, (int)p.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
+  const int mbeg = split * p.iters_per_split * 64;  // host splits in 64-row units
+  const int mend_raw = mbeg + p.iters_per_split * 64;
+  const int mend = mend_raw < p.M ? mend_raw : p.M;
+  const int nit = mend > mbeg ? (mend - mbeg + SR - 1) / SR : 0;
+  const int OHW = p.OH * p.OW;
+
+  int d_row[DI];
+  uint32_t d_off[DI];
+  bool d_cok[DI];
+#pragma unroll
+  for (int j = 0; j < DI; ++j) {
+    const int r = (j * NW + wid) * RPD + lane / CPD;
+    const int col = co0 + tr_swz<BCO>(r, (lane % CPD) * 8);
+    d_row[j] = r;
+    d_cok[j] = col < p.N;
+    d_off[j] = (uint32_t)(((size_t)(mbeg + r) * p.N + col) * 2);
+  }
+  const uint32_t dstep = (uint32_t)(SR * p.N * 2);
+  int x_row[XI], x_ci[XI], x_ihb[XI], x_iwb[XI], xn[XI], xoh[XI], xow[XI];
+  bool x_kok[XI];
+#pragma unroll
+  for (int j = 0; j < XI; ++j) {
+    const int r = (j * NW + wid) * RPX + lane / CPX;
+    const int kk = k0 + tr_swz<BKK>(r, (lane % CPX) * 8);
+    x_row[j] = r;
+    x_kok[j] = kk < p.K;
+    const int tap = x_kok[j] ? kk / p.C : 0;
+    x_ci[j] = kk - tap * p.C;
+    const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+    x_ihb[j] = p.ih0 + kh * p.dh;
+    x_iwb[j] = p.iw0 + kw * p.dw;
+    const int m = mbeg + r;
+    xn[j] = m / OHW;
+    const int rem = m - xn[j] * OHW;
+    xoh[j] = rem / p.OW;
+    xow[j] = rem - xoh[j] * p.OW;
+  }
+  const int dn = SR / OHW, dr = SR - dn * OHW;
+  const int doh = dr / p.OW, dow = dr - doh * p.OW;
+  const int cstride = p.C * 2;
+
+  auto issue = [&](int it, int buf) {
+    const int mb = mbeg + it * SR;
+#pragma unroll
+    for (int j = 0; j < DI; ++j) {
+      const bool ok = mb + d_row[j] < mend && d_cok[j];
+      dma16_opaque(rd, Ds + buf * SR * BCO + (j * NW + wid) * RPD * BCO,
+                   ok ? d_off[j] : p.dy_bytes);
+      d_off[j] += dstep;
+    }
+#pragma unroll
+    for (int j = 0; j < XI; ++j) {
+      const int ih = (int)__umul24((unsigned)xoh[j], (unsigned)p.ish) + x_ihb[j];
+      const int iw = (int)__umul24((unsigned)xow[j], (unsigned)p.isw) + x_iwb[j];
+      const bool ok = mb + x_row[j] < mend && x_kok[j] && (unsigned)ih < (unsigned)p.IH &&
+                      (unsigned)iw < (unsigned)p.IW;
+      const uint32_t pix =
+          __umul24(__umul24((unsigned)xn[j], (unsigned)p.IH) + (unsigned)ih, (unsigned)p.IW) +
+          (unsigned)iw;
+      const uint32_t off = ok ? __umul24(pix, (unsigned)cstride) + (uint32_t)(x_ci[j] * 2)
+                              : p.x_bytes;
+      dma16_opaque(rx, Xs + buf * SR * BKK + (j * NW + wid) * RPX * BKK, off);
+      int ow = xow[j] + dow, oh = xoh[j] + doh, n = xn[j] + dn;
+      if (ow >= p.OW) { ow -= p.OW; ++oh; }
+      if (oh >= p.OH) { oh -= p.OH; ++n; }
+      xow[j] = ow; xoh[j] = oh; xn[j] = n;
+    }
+  };
+
+  f32x4 acc[BCO / WM / 16][BKK / WN / 16];
+#pragma unroll
+  for (int i = 0; i < BCO / WM / 16; ++i)
+#pragma unroll
+    for (int j = 0; j < BKK / WN / 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (j < nit) issue(j, j);
+  int cur = 0;
+  for (int it = 0; it < nit; ++it) {
+    // steps it+1 .. min(it+NST-2, nit-1) may stay in flight; step it must have landed
+    const int ahead = min(NST - 2, nit - 1 - it);
+    if (ahead >= NST - 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (NST - 2)) : "memory");
+    else if (NST > 3 && ahead == 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * 2) : "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // step it landed for every wave; buffer (it-1) % NST is free
+    if (it + NST - 1 < nit) {
+      const int nb = cur == 0 ? NST - 1 : cur - 1;  // (it + NST - 1) % NST
+      issue(it + NST - 1, nb);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    wgrad_mma<BCO, BKK, WM, WN, SR / 32>(Ds + cur * SR * BCO, Xs + cur * SR * BKK, acc);
+    __builtin_amdgcn_s_setprio(0);
+    cur = cur + 1 == NST ? 0 : cur + 1;
+  }
+  wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
 }
 
 // Weight gradient of a 3x3 / stride-1 / pad-1 convolution (16x16 / 32x32, C in {64, 128}) with
@@ -2231,10 +1995,6 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
         out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
       }
     }
-  int kb[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) kb[t] = t * C + ci0;
-  wgrad_finish<9>(p, smem, tile, co0, B, kb, B);
 }
 
 // out[co][tap][ci < Creal] (+)= Σ_s partial[s*stride][co][tap*C + ci]   (slab stride in slabs)
@@ -2414,47 +2174,26 @@ void launch_patch(const IgemmArgs& a, hipStream_t s) {
   }
 }
 
-template <int EPI, int PRO>
-void launch_ppatch_t(const IgemmArgs& a0, hipStream_t s) {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        ncu <= 0)
-      ncu = 256;
-  }
-  IgemmArgs a = a0;
-  a.nMb = a.M / 256;
-  a.nNb = 1;
-  const int grid = a.nMb < ncu ? a.nMb : ncu;  // one resident block per CU (LDS-bound)
-  hipLaunchKernelGGL((igemm_ppatch<EPI, PRO>), dim3(grid), dim3(512), PP_LDS, s, a);
-  HIP_CHECK_LAUNCH();
-}
-
-void launch_ppatch(const IgemmArgs& a, hipStream_t s) {
-  const bool pro = a.pro_sc != nullptr;
-  switch (a.epi_mode) {
-    case 1: pro ? launch_ppatch_t<1, 1>(a, s) : launch_ppatch_t<1, 0>(a, s); break;
-    case 2: pro ? launch_ppatch_t<2, 1>(a, s) : launch_ppatch_t<2, 0>(a, s); break;
-    case 3: pro ? launch_ppatch_t<3, 1>(a, s) : launch_ppatch_t<3, 0>(a, s); break;
-    case 4:
-      if (a.stats2 != nullptr)
-        pro ? launch_ppatch_t<5, 1>(a, s) : launch_ppatch_t<5, 0>(a, s);
-      else
-        pro ? launch_ppatch_t<4, 1>(a, s) : launch_ppatch_t<4, 0>(a, s);
-      break;
-    default: pro ? launch_ppatch_t<0, 1>(a, s) : launch_ppatch_t<0, 0>(a, s); break;
-  }
-}
 
 template <int BM, int BN, int WM, int WN, int NST = 2>
 void launch_glds(const IgemmArgs& a, hipStream_t s) {
-  if (a.pro_d != nullptr) {  // BN-backward prologue (PRO 2): plain or mode-3 epilogue
+  if (a.pro_d != nullptr) {  // BN-backward prologue (PRO 2): plain, mode-3 or mode-4 epilogue
     if constexpr (NST == 2) {
       if (a.epi_mode == 3)
         launch_glds_t<BM, BN, WM, WN, 2, 3, NST>(a, s);
-      else
+      else if (a.epi_mode == 4) {
+        // (the 256 x 256 tile with both fusions drains its DMA pipeline: not instantiated,
+        // igemm_bnb_epi4_ok rejects it)
+        if constexpr (BM * BN <= 256 * 128) {
+          if (a.stats2 != nullptr)
+            launch_glds_t<BM, BN, WM, WN, 2, 5, NST>(a, s);
+          else
+            launch_glds_t<BM, BN, WM, WN, 2, 4, NST>(a, s);
+        } else {
+          fprintf(stderr, "igemm: BN-backward prologue + mode-4 epilogue on a 256x256 tile\n");
+          abort();
+        }
+      } else
         launch_glds_t<BM, BN, WM, WN, 2, 0, NST>(a, s);
     } else {
       fprintf(stderr, "igemm: 3-stage LDS-DMA variant with the BN-backward prologue\n");
@@ -2502,9 +2241,13 @@ void launch_glds(const IgemmArgs& a, hipStream_t s) {
 // compile-time fusion modes (prologue x epilogue), so each launch carries only its own work
 template <int BM, int BN, int WM, int WN>
 void launch_igemm(const IgemmArgs& a, hipStream_t s) {
-  if (a.pro_d != nullptr) {  // BN-backward prologue: only with a plain or mode-3 epilogue
+  if (a.pro_d != nullptr) {  // BN-backward prologue: plain, mode-3 or mode-4 epilogue
     if (a.epi_mode == 3)
       launch_igemm_t<BM, BN, WM, WN, 2, 3>(a, s);
+    else if (a.epi_mode == 4 && a.stats2 != nullptr)
+      launch_igemm_t<BM, BN, WM, WN, 2, 5>(a, s);
+    else if (a.epi_mode == 4)
+      launch_igemm_t<BM, BN, WM, WN, 2, 4>(a, s);
     else
       launch_igemm_t<BM, BN, WM, WN, 2, 0>(a, s);
     return;
@@ -2552,6 +2295,18 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+template <int BCO, int BKK, int WM, int WN, int SR, int NST>
+void launch_wgrad_pipe(const WgradArgs& a0, hipStream_t s) {
+  WgradArgs a = a0;
+  a.nCo = (a.N + BCO - 1) / BCO;
+  a.nKk = (a.K + BKK - 1) / BKK;
+  const int grid = a.nCo * a.nKk * a.splits;
+  const size_t lds = (size_t)NST * SR * (BCO + BKK) * 2;
+  hipLaunchKernelGGL((wgrad_pipe<BCO, BKK, WM, WN, SR, NST>), dim3(grid), dim3(64 * WM * WN),
+                     lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
 template <int BCO, int BKK, int WM, int WN, int NST = 2>
 void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
@@ -2578,17 +2333,16 @@ constexpr int IG_VARIANTS[][2] = {{128, 128}, {256, 64}, {128, 64}, {64, 128}, {
                                   {256, 128}, {128, 128}, {128, 256},
                                   {256, 64}, {256, 128},
                                   {256, 64}, {128, 256}, {256, 128},
-                                  {256, 64}, {128, 256}, {256, 128}, {128, 128}};
+                                  {128, 256}, {256, 128}};
 constexpr int IG_GLDS0 = 7;   // LDS-DMA kernel from here on
 constexpr int IG_GLDS3 = 12;  // ... with three LDS stages (no BN-apply prologue)
 constexpr int IG_PATCH0 = 15;  // 3x3 stride-1 kernel with an LDS-resident input patch
 constexpr int IG_GLDS8W = 17;  // 2-stage LDS-DMA, 256 x 64 tile on 8 waves (memory-bound 1x1)
 // 18, 19: 2-stage LDS-DMA, one wave column (WN = 1): the BN-apply prologue runs on the A
 // fragments in registers (the short-K 1x1 expansion convs, conv3 of a bottleneck)
-constexpr int IG_PPATCH = 20;  // persistent 3x3 patch kernel, resident weights (C = N = 64, 32x32)
-// 21, 22: single-stage LDS-DMA tiles, 2 blocks per CU (short-K 1x1 convs: one block's loads and
+// 20, 21: single-stage LDS-DMA tiles, 2 blocks per CU (short-K 1x1 convs: one block's loads and
 // epilogue under the other's MFMAs instead of a second LDS stage); BN-apply prologue only
-constexpr int IG_GLDS1 = 21;
+constexpr int IG_GLDS1 = 20;
 // variants >= WG_GLDS0 are the LDS-DMA kernel (wgrad_glds): no prologues, C % 64 == 0
 // {BCO, BKK, target resident blocks}: the split-M count is chosen to fill the chip with about
 // that many blocks; every split costs an fp32 N x K slab written here and re-read by the
@@ -2600,14 +2354,15 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {128, 64, 512},  {128, 128, 256}, {64, 128, 512},
                                   {256, 128, 256}, {64, 64, 256},
                                   {64, 128, 768}, {128, 64, 768},
-                                  {128, 128, 512}, {256, 128, 512}};
+                                  {256, 256, 256}, {256, 128, 256}, {128, 256, 256}};
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 // wgrad_tn with loads two steps ahead (DEEP): the 64 x 128 / 128 x 64 tiles gain 10-17 % on the
 // 3x3 / 1x1 weight gradients (tools/wgrad_probe.py); the 128 x 128 and 256 x 64 DEEP tiles spill
 // at the 256-VGPR cap of two blocks per CU and lose (not instantiated)
 constexpr int WG_DEEP0 = 18;
-constexpr int WG_GLDS1 = 20;  // 20, 21: single-stage LDS-DMA tiles, 2 blocks per CU
+// 20-22: wgrad_pipe (32-row steps, 4-5 LDS stages with all but one in flight), no prologues
+constexpr int WG_PIPE0 = 20;
 
 
 // -------------------------------------------------- fused 1x1 backward: dgrad + wgrad in one pass
@@ -2875,7 +2630,7 @@ bool igemm_patch_ok(const ConvGeom& g) {
 // block-output prologue (PRO 3): 2-stage LDS-DMA tiles whose doubled A staging fits the LDS,
 // on 1x1 / stride-1 / unpadded / direct-output convolutions (A row m = output row m)
 bool igemm_dual_ok(int v, const ConvGeom& g) {
-  if (!((v >= IG_GLDS0 && v < IG_GLDS3) || (v >= IG_GLDS8W && v < IG_PPATCH)) ||
+  if (!((v >= IG_GLDS0 && v < IG_GLDS3) || (v >= IG_GLDS8W && v < IG_GLDS1)) ||
       !igemm_glds_ok(g, true, false))
     return false;
   const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
@@ -2888,18 +2643,14 @@ bool igemm_dual_ok(int v, const ConvGeom& g) {
   return lds <= 160 * 1024;
 }
 
-bool igemm_ppatch_ok(const ConvGeom& g) {
-  return igemm_patch_ok(g) && g.C == 64 && g.N == 64 && g.OW == 32;
-}
 
-bool igemm_variant_is_patch(int v) { return (v >= IG_PATCH0 && v < IG_GLDS8W) || v == IG_PPATCH; }
+bool igemm_variant_is_patch(int v) { return v >= IG_PATCH0 && v < IG_GLDS8W; }
 
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
   // patch kernel: BN-apply prologue but no BN-backward one
   if (v >= IG_PATCH0 && v < IG_GLDS8W) return !bn_bwd_pro && igemm_patch_ok(g);
-  if (v == IG_PPATCH) return !bn_bwd_pro && igemm_ppatch_ok(g);
   if (v >= IG_GLDS1) return !bn_bwd_pro && igemm_glds_ok(g, pro, false);
   if (v >= IG_GLDS3 && v < IG_PATCH0 && (pro || bn_bwd_pro)) return false;
   if (bn_bwd_pro) {  // PRO 2 stages dY and x: doubled A staging + a 3 x C table must fit
@@ -2935,8 +2686,6 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_c2 = f.epi_c2; a.epi_mi2 = f.epi_mi2; a.stats2 = f.stats2;
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
-  a.tail = f.tail;
-  a.stats_groups = f.stats_groups;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
   if (a.pro_out != nullptr
           ? !igemm_dual_ok(variant, g)
@@ -2958,10 +2707,8 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
     case 17: launch_glds<256, 64, 8, 1>(a, s); break;
     case 18: launch_glds<128, 256, 4, 1>(a, s); break;
     case 19: launch_glds<256, 128, 8, 1>(a, s); break;
-    case 20: launch_ppatch(a, s); break;
-    case 21: launch_glds<128, 256, 2, 2, 1>(a, s); break;
-    case 22: launch_glds<256, 128, 2, 2, 1>(a, s); break;
-    case 23: launch_glds<128, 128, 2, 2, 1>(a, s); break;
+    case 20: launch_glds<128, 256, 2, 2, 1>(a, s); break;
+    case 21: launch_glds<256, 128, 2, 2, 1>(a, s); break;
     case 0: launch_igemm<128, 128, 2, 2>(a, s); break;
     case 1: launch_igemm<256, 64, 4, 1>(a, s); break;
     case 2: launch_igemm<128, 64, 2, 2>(a, s); break;
@@ -2972,21 +2719,14 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   }
 }
 
-void igemm_tail_plan(int nmb_seg, int* gr, int* ngrp) {
-  int g = 32;
-  while ((nmb_seg + g - 1) / g > 64) g *= 2;  // <= 64 level-2 rows per segment
-  *gr = g;
-  *ngrp = (nmb_seg + g - 1) / g;
-}
-int igemm_tail_ticket_words(int nNb, int S, int ngrp) { return nNb * S * ngrp + nNb; }
 
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
-bool wgrad_variant_glds(int v) { return (v >= WG_GLDS0 && v < WG_PATCH0) || v >= WG_GLDS1; }
+bool wgrad_variant_glds(int v) { return (v >= WG_GLDS0 && v < WG_PATCH0) || v >= WG_PIPE0; }
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
   if (v == WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
-  if (v >= WG_GLDS1) return !dy_pro && igemm_glds_ok(g, pro, false);
+  if (v >= WG_PIPE0) return !dy_pro && !pro && igemm_glds_ok(g, false, false);
   if (v >= WG_DEEP0) return true;  // register-staged: every prologue
   // wgrad_glds has the X-operand BN-apply prologue only (no dY BN-backward prologue)
   return v < WG_GLDS0 || (!dy_pro && igemm_glds_ok(g, pro, false));
@@ -3036,13 +2776,9 @@ int wgrad_tiles(const ConvGeom& g, int variant) {
   return ((g.N + bco - 1) / bco) * ((K + bkk - 1) / bkk);
 }
 
-bool wgrad_inkernel_reduce_ok(const ConvGeom& g, int Creal) {
-  return Creal == g.C && (g.KH * g.KW * g.C) % 4 == 0;
-}
-
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
                 float* partial, int splits, float* out, int Creal, float beta,
-                const ConvFusion& f, int variant, hipStream_t s, int* tickets) {
+                const ConvFusion& f, int variant, hipStream_t s) {
   WgradArgs a{};
   a.dY = dY; a.X = X; a.partial = partial;
   a.M = g.Nb * g.OH * g.OW; a.N = g.N; a.K = g.KH * g.KW * g.C;
@@ -3059,12 +2795,6 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.pro_relu = f.pro_relu; a.pro_S = f.pro_S > 0 ? f.pro_S : 1;
   a.dY2 = f.dY2; a.dp_coef = f.dp_coef; a.dp_seg_rows = f.dp_seg_rows > 0 ? f.dp_seg_rows : a.M;
   a.dp_S = f.dp_S > 0 ? f.dp_S : 1;
-  const bool inkernel = tickets != nullptr && wgrad_inkernel_reduce_ok(g, Creal);
-  if (inkernel) {
-    a.tickets = tickets;
-    a.out = out;
-    a.beta = beta;
-  }
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
   if (!wgrad_variant_ok(variant, g, a.pro_sc != nullptr, a.dY2 != nullptr)) {
     fprintf(stderr, "wgrad: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
@@ -3107,8 +2837,9 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     }
     case 18: launch_wgrad<64, 128, 2, 2, true>(a, s); break;
     case 19: launch_wgrad<128, 64, 2, 2, true>(a, s); break;
-    case 20: launch_wgrad_glds<128, 128, 2, 2, 1>(a, s); break;
-    case 21: launch_wgrad_glds<256, 128, 2, 2, 1>(a, s); break;
+    case 20: launch_wgrad_pipe<256, 256, 2, 4, 32, 4>(a, s); break;
+    case 21: launch_wgrad_pipe<256, 128, 4, 2, 32, 5>(a, s); break;
+    case 22: launch_wgrad_pipe<128, 256, 2, 4, 32, 5>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;
@@ -3116,7 +2847,6 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 5: launch_wgrad<256, 64, 2, 2>(a, s); break;
     default: launch_wgrad<64, 64, 2, 2>(a, s); break;
   }
-  if (inkernel) return;  // the kernel's last arrivers wrote ``out``
   const int K = a.K;
   const size_t n4 = (size_t)a.N * K / 4;
   int sstride = 1, count = splits;

@@ -17,40 +17,6 @@ struct ConvGeom {
 };
 
 // ---- conv.hip
-// BatchNorm finalize in the conv kernel's tail (bn_tail.h): cross-rank exchange + finalize
-// parameters, and the two-level last-arriver plan over the launch's row-blocks.
-struct IpcX {
-  uint64_t* const* peers = nullptr;  // [world] arena bases (own included); nullptr = no exchange
-  uint64_t* own = nullptr;
-  long long site = 0;                // word offset of this BatchNorm's region
-  unsigned* epoch = nullptr;         // per-64-channel-group counters of the site
-  int* err = nullptr;
-  int world = 1, rank = 0;
-};
-struct BnFin {
-  int mode = 0;  // 1 forward finalize, 2 backward finalize
-  int S = 1, C = 0;
-  float count = 1.f, eps = 1e-5f, momentum = 0.1f;
-  float* rm = nullptr;
-  float* rv = nullptr;
-  float* mi = nullptr;         // mode 1 out / mode 2 in: [2][S][C] mean, invstd
-  int64_t* nbt = nullptr;
-  const float* gamma = nullptr;
-  const float* beta = nullptr;
-  float* ss = nullptr;         // mode 1 out: [2][S][C] scale, shift
-  float* dgamma = nullptr;     // mode 2 out (rank-local sums)
-  float* dbeta = nullptr;
-  float* coef = nullptr;       // mode 2 out: [3][S][C]
-  IpcX ipc;
-};
-struct BnTailArgs {
-  int on = 0;                  // 0 off, else fin.mode
-  int nmb_seg = 0;             // row-blocks per segment (seg_rows / BM)
-  int gr = 1, ngrp = 1;        // level-1 group size (row-blocks) and groups per segment
-  unsigned* tick = nullptr;    // [nNb][S][ngrp] level-1 + [nNb] level-2 (zeroed, self-resetting)
-  float* ws = nullptr;         // level-2 rows [S][ngrp][2][N]
-  BnFin fin;
-};
 // Optional fusions around the implicit GEMM (all pointers nullable / mode 0 = off).
 struct ConvFusion {
   const float* pro_sc = nullptr;  // A/X-operand prologue: a = relu?(x*sc[seg][c] + sh[seg][c])
@@ -85,11 +51,7 @@ struct ConvFusion {
   int seg_rows = 0;               // rows per segment of the output (stats remap, mode 3)
   int stats_seg_blocks = 0;       // >0: segment-major stats rows (see conv.hip)
   int stats_base = 0;
-  BnTailArgs tail;                // BatchNorm finalize in the kernel's last blocks (bn_tail.h)
-  int stats_groups = 0;           // >0: atomic partials in [S][G][2][N] replica rows (conv.hip)
 };
-int igemm_tail_ticket_words(int nNb, int S, int ngrp);
-void igemm_tail_plan(int nmb_seg, int* gr, int* ngrp);
 
 int igemm_num_variants();
 int igemm_variant_bm(int v);
@@ -113,7 +75,7 @@ bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro);
 int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,
                 float* partial, int splits, float* out, int Creal, float beta,
-                const ConvFusion& f, int variant, hipStream_t s, int* tickets = nullptr);
+                const ConvFusion& f, int variant, hipStream_t s);
 // fused 1x1 backward (dgrad + wgrad + BN2-backward partials in one pass, Co = 256, Ci = 64)
 size_t conv1x1_bwd_dual_lds();
 void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, const uint16_t* X,
@@ -124,7 +86,6 @@ void wgrad_reduce_slabs(float* partial, int splits, float* out, size_t n, float 
                         hipStream_t s);
 // output tiles of a weight-gradient launch (ticket words of the in-kernel split reduction)
 int wgrad_tiles(const ConvGeom& g, int variant);
-bool wgrad_inkernel_reduce_ok(const ConvGeom& g, int Creal);
 // one dgrad weight transform (see weight_transform_batch): Wt[ci][khs][kws][co] =
 // W[co][kh0 + khs*sh][kw0 + kws*sw][ci]; blocks [blk0, blk0 + nblk) of the batch launch
 struct WtDesc {
@@ -168,7 +129,6 @@ struct BnReduceFusedParams {
   float* dgamma = nullptr;
   float* dbeta = nullptr;
   float* coef = nullptr;
-  int zero_after = 0;  // direct mode: zero the partial rows once read (atomic accumulators)
   // cross-rank exchange over IPC-mapped peer arenas (modes 1 / 2 at world > 1, see bn.hip)
   uint64_t* const* ipc_peers = nullptr;  // device array [world] of arena bases (own included)
   uint64_t* ipc_own = nullptr;           // this rank's arena base

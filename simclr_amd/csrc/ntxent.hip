@@ -287,21 +287,10 @@ __global__ void k_reduce_loss(const float* __restrict__ loss, int R, float scale
 // between) and at most 4096 (the split partials grow with the count).  tools/ntxent_bench.py,
 // R = 1024: at 8192 global negatives (8 ranks) the fixed 512-block rule took 85 + 107 + 327 µs
 // (forward, column and row gradient passes), this one ~57 + 78 + 94; at 1024 columns it keeps
-// 512.  SIMCLR_NTX_BLOCKS=N forces a fixed block target (experiments).
-int ntx_fixed_blocks() {
-  static const int t = [] {
-    const char* e = getenv("SIMCLR_NTX_BLOCKS");
-    return e ? atoi(e) : 0;
-  }();
-  return t;
-}
-
+// 512.
 int splits_for(int tiles, int ptiles, int tiles_per_block = 8) {
-  long target = ntx_fixed_blocks();
-  if (target <= 0) {
-    target = (long)tiles * ptiles / tiles_per_block;
-    target = target < 512 ? 512 : (target > 4096 ? 4096 : target);
-  }
+  long target = (long)tiles * ptiles / tiles_per_block;
+  target = target < 512 ? 512 : (target > 4096 ? 4096 : target);
   int s = (int)((target + tiles - 1) / tiles);
   if (s > ptiles) s = ptiles;
   if (s < 1) s = 1;

@@ -119,14 +119,19 @@ class _BlockTape:
 
 
 # persistent blocks per view segment of the fused 1x1 backward (2 segments: 2x this many blocks)
-_BWD1X1_BPS = int(os.environ.get("SIMCLR_BWD1X1_BPS", "128"))
+_BWD1X1_BPS = 128
 
 # bit 8 of the igemm epilogue mode: the residual operand is stride-2 subsampled (conv.hip)
 _EPI_SUB = 256
 
 
 class FusedStages:
-    """Executor over ``resnet.layer1..layer4`` (modules stay the parameter / state owners)."""
+    """Executor over ``resnet.layer1..layer4`` (modules stay the parameter / state owners).
+
+    The fusion switches below are instance attributes (tests and A/B tools flip them on a built
+    executor); the class attribute ``BLOCK_OUT_PROLOGUE`` is the default of new executors."""
+
+    BLOCK_OUT_PROLOGUE = True
 
     def __init__(self, resnet: torch.nn.Module, segments: int = 2):
         from .resnet import BasicBlock, Bottleneck
@@ -137,8 +142,11 @@ class FusedStages:
         self.dual_launches = 0
         self.out_apply_calls = 0
         # BN backward of a bottleneck's conv3 inside conv3's dgrad/wgrad operand prologues
-        self.bnb_prologue = os.environ.get("SIMCLR_BNB_PROLOGUE", "1") != "0"
-        self._bnb_max_cin = int(os.environ.get("SIMCLR_BNB_MAX_CIN", "128"))
+        # (only up to 128 input channels: measured net loss or break-even above, r2 log)
+        self.bnb_prologue = True
+        self._bnb_max_cin = 128
+        # BN1's backward in conv1's operand prologues as well: measured +0.85 ms/step (r4 log)
+        self.lazy_bn1 = False
         # weight gradients on a second stream (forked after each conv's dY is final, joined at
         # the end of the backward): they only feed the flat gradient buffer, so they overlap the
         # dgrad / BatchNorm chain that the next layer's gradient depends on
@@ -151,39 +159,17 @@ class FusedStages:
         # the even positions) and added by conv1's dgrad epilogue through the subsampled-residual
         # mode — instead of zero-filling a full-resolution tensor (0.9 GB/step of fills at
         # ResNet-50 CIFAR) and re-reading it whole
-        self.compact_ds = os.environ.get("SIMCLR_COMPACT_DS", "1") != "0"
-        # BN1-apply + ReLU of a bottleneck's 3x3 conv2 input in the patch kernels' prologue:
-        # off by default — the in-LDS pass over the halo'd patch costs more than the apply pass
-        # it saves (tools/patch_pro_bench.py: layer1 fwd +48 µs / wgrad +36 µs vs 42 µs apply)
-        self.patch_prologue = os.environ.get("SIMCLR_PATCH_PROLOGUE", "0") == "1"
+        self.compact_ds = True
         self._branch = None
         # a block's output (BN3 + shortcut + ReLU) formed inside the next block's conv1 prologue
-        # instead of a separate pass that conv1 re-reads.  SIMCLR_BLOCK_OUT_PROLOGUE: 0 = off,
-        # N >= 1 = on for blocks whose maps are at least N x N (1 = every block, the default:
-        # since the prologue kernels keep their DMA pipelined it wins at every stage —
-        # 24.06 -> 23.80 ms/step A/B, r2 optimisation log)
-        v = os.environ.get("SIMCLR_BLOCK_OUT_PROLOGUE", "1")
-        self.block_out_min_hw = int(v) if v.isdigit() else 1
-        self.block_out_prologue = self.block_out_min_hw > 0
-        # BatchNorm reduce + finalize in the producing conv kernel's last blocks (csrc/bn_tail.h)
-        # instead of a separate reduce launch per BatchNorm.  Off by default and compiled only
-        # by SIMCLR_BUILD_BN_TAIL=1 builds: every block has to drain its stores (incl. the
-        # nontemporal output tile) before its ticket, which costs more than the launches it
-        # saves (24.33 -> 25.59 ms/step A/B, r2 log)
-        self.bn_tail = os.environ.get("SIMCLR_BN_TAIL", "0") == "1"
-        # SIMCLR_STATS_GROUPS=G: conv-epilogue BatchNorm partials accumulated with float atomics
-        # into G replica rows per segment (persistent per-BatchNorm buffers, zeroed by the
-        # reduce that reads them), so the reduce is one pass over S·G rows instead of a sliced
-        # two-level pass over one row per row-block.  Off by default: measured neutral (24.10 vs
-        # 24.07 ms/step — the reduce launch's cost is its dispatch, not its reads) and atomic
-        # order is not reproducible; deterministic runs never use it.
+        # instead of a separate pass that conv1 re-reads, at every stage (the prologue kernels
+        # keep their DMA pipelined: 24.06 -> 23.80 ms/step A/B, r2 optimisation log)
+        self.block_out_min_hw = 1
+        self.block_out_prologue = type(self).BLOCK_OUT_PROLOGUE
         # a bottleneck's conv3 backward at Ci = 64 / Co = 256 (ResNet-50 layer1) as ONE fused
         # pass (conv.hip conv1x1_bwd_dual): dgrad + BN2 mask / partials + weight gradient, so the
         # 0.5-1 GB output gradient is read once instead of once per pass
-        self.fused_bwd1x1 = os.environ.get("SIMCLR_FUSED_BWD1X1", "1") != "0"
-        g = os.environ.get("SIMCLR_STATS_GROUPS", "0")
-        self.stats_groups = int(g) if g.isdigit() else 0
-        self._accs = {}
+        self.fused_bwd1x1 = True
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -231,53 +217,15 @@ class FusedStages:
         return True
 
     # ------------------------------------------------------------------ building blocks
-    def _groups(self) -> int:
-        """Replica rows per segment for atomic BatchNorm partials (0: one row per row-block)."""
-        if self.stats_groups <= 0 or torch.are_deterministic_algorithms_enabled():
-            return 0
-        return min(self.stats_groups, 64)
-
-    def _acc(self, key, S: int, G: int, C: int, dev) -> torch.Tensor:
-        """Persistent zeroed [S][G][2][C] accumulator of one BatchNorm site (the reduce that
-        reads it zeroes it again).  Allocated on first use — the eager warm-up steps, before any
-        hipGraph capture."""
-        n = S * G * 2 * C
-        t = self._accs.get(key)
-        if t is None or t.numel() != n or t.device != dev:
-            t = torch.zeros((n,), device=dev, dtype=torch.float32)
-            self._accs[key] = t
-        return t
-
-    def _tail_ok(self, st, C: int, S: int) -> bool:
-        return (getattr(self, "bn_tail", False) and C % 64 == 0 and S <= 2
-                and (not st.comm or st.ipc is not None))
-
-    def _tail_spec(self, bn, mode: int, S: int, st, slot: int, count: float, mi, ss=None,
-                   dgamma=None, dbeta=None, coef=None):
-        """(mode, tensors, floats, ints) of a conv-tail BatchNorm finalize (ops/conv_hip.py)."""
-        C = bn.num_features
-        t = [mi, ss,
-             bn.running_mean if mode == 1 else None, bn.running_var if mode == 1 else None,
-             bn.num_batches_tracked if mode == 1 else None,
-             bn.weight.detach(), bn.bias.detach() if mode == 1 else None, dgamma, dbeta, coef]
-        ints = [0, 1, 0, slot]
-        if st.ipc is not None:
-            kw = st.ipc.kwargs(site_key(bn, "fwd" if mode == 1 else "bwd"), S, C)
-            t += [kw["ipc_peers"], kw["ipc_arena"], kw["ipc_epoch"], kw["ipc_err"]]
-            ints = [kw["ipc_site"], kw["world"], kw["rank"], slot]
-        return (mode, t, [count, bn.eps if mode == 1 else 0.0,
-                          bn.momentum if mode == 1 else 0.0], ints)
-
     def _conv_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int,
-                  dual=None, st=None, slot: int = 0):
+                  dual=None):
         """a = conv(pro(x)) with BN statistics partials in the epilogue.
 
         ``dual = (aL, ss, res, rss, out, mask)``: the input is the previous block's output,
         formed in this conv's prologue from that block's conv3 activation ``aL`` and residual
         ``res`` and written to ``out`` / ``mask`` by the same kernel (``xn`` is ``out``).
-        Returns (a, partials, blocks per segment, bn state): with ``st`` given and the conv
-        tail applicable, the conv's last blocks also finalize ``cs.bn`` (state returned,
-        partials None); otherwise the caller reduces the partials (``_bn_fwd``)."""
+        Returns (a, partials, blocks per segment); the caller reduces the partials
+        (``_bn_fwd``)."""
         Nb, H, W, C = xn.shape
         Co = cs.conv.out_channels
         OH = (H + 2 * cs.pad - cs.k) // cs.stride + 1
@@ -295,35 +243,9 @@ class FusedStages:
             pro = (pro_ss[0], pro_ss[1], M // S, True)
         v = igemm_choose(ops, A, w, a, g, want_stats=True, pro=pro, seg_rows=M // S, dual=dl)
         bm = ops.igemm_variant_bm(v)
-        G = self._groups()
-        use_tail = st is not None and self._tail_ok(st, Co, S)
-        if G and not use_tail:  # atomic replica partials (see __init__)
-            stats = self._acc((id(cs.bn), "fwd"), S, G, Co, xn.device)
-            igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl, seg_rows=M // S,
-                         stats_groups=G)
-            return a, stats, -G, None  # negative: accumulator rows (reduce with zero_after)
         stats = torch.empty(((M // bm) * 2 * Co,), device=xn.device, dtype=torch.float32)
-        tail, bs = None, None
-        if st is not None and self._tail_ok(st, Co, S):
-            bn = cs.bn
-            mi = torch.empty((2 * S * Co,), device=xn.device, dtype=torch.float32)
-            ss = torch.empty((2 * S * Co,), device=xn.device, dtype=torch.float32)
-            count = float((M // S) * st.world_size)
-            tail = self._tail_spec(bn, 1, S, st, slot, count, mi, ss=ss)
-            bs = _BNState(mi, ss.view(2, S * Co), count)
-        igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl, tail=tail,
-                     seg_rows=M // S if tail is not None else 0)
-        return a, stats, M // bm // S, bs
-
-    def _patch_pro_ok(self, xn, cs: _ConvSpec) -> bool:
-        """3x3 / stride 1 / pad 1 conv at 16x16 or 32x32 with 64 / 128 input channels: the patch
-        kernels (forward igemm_patch, weight-gradient wgrad_patch) take the previous BatchNorm's
-        apply + ReLU in their prologue, so its output is never materialised."""
-        if not (getattr(self, "patch_prologue", False) and xn.is_cuda):
-            return False
-        Nb, H, W, C = xn.shape
-        return (cs.k == 3 and cs.stride == 1 and cs.pad == 1 and H == W and H in (16, 32)
-                and C in (64, 128))
+        igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl)
+        return a, stats, M // bm // S
 
     def _dual_ok(self, ops, xn, cs: _ConvSpec, S: int) -> bool:
         """Can ``cs`` (a block's conv1) form its input — the previous block's output — in its
@@ -353,44 +275,21 @@ class FusedStages:
         mi = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ss = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
         ipc = st.ipc
-        zero = nblk_seg < 0  # atomic accumulator rows: read once, zeroed by the reduce
-        nblk_seg = abs(nblk_seg)
         if not st.comm or ipc is not None:
             # one launch: reduce + finalize (last-arriver); at world > 1 the IPC statistics
             # exchange runs inside it (comm/ipc.py)
             ops.bn_reduce_fused(partial, nblk_seg, S, C, 1, None, count, bn.eps, bn.momentum,
                                 bn.running_mean, bn.running_var, mi, bn.num_batches_tracked,
                                 bn.weight.detach(), bn.bias.detach(), ss, None, None, None, slot,
-                                **(ipc.kwargs(site_key(bn, "fwd"), S, C) if ipc is not None else {}),
-                                zero_after=zero)
+                                **(ipc.kwargs(site_key(bn, "fwd"), S, C) if ipc is not None else {}))
         else:
             stats = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats, ticket_slot=slot,
-                                zero_after=zero)
+            ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, stats, ticket_slot=slot)
             _allreduce(stats, st, branch=slot == 1)
             ops.bn_finalize(stats, S, C, count, bn.eps, bn.momentum, bn.running_mean,
                             bn.running_var, mi, bn.num_batches_tracked, bn.weight.detach(),
                             bn.bias.detach(), ss)
         return _BNState(mi, ss.view(2, S * C), count)
-
-    def _bn_grad_targets(self, bn):
-        """(dγ out, dβ out, finish): the flat-store slots (finish marks them ready for the
-        bucketed all-reduce) or temporaries handed to ``_deliver_grad`` by finish."""
-        gslot = getattr(bn.weight, "_slot", None)
-        bslot = getattr(bn.bias, "_slot", None)
-        if gslot is not None and bslot is not None:
-            def finish():
-                gslot.store.mark_ready(gslot.index)
-                bslot.store.mark_ready(bslot.index)
-            return gslot.grad, bslot.grad, finish
-        C = bn.num_features
-        dg = torch.empty((C,), device=bn.weight.device, dtype=torch.float32)
-        db = torch.empty((C,), device=bn.weight.device, dtype=torch.float32)
-
-        def finish_tmp():
-            _deliver_grad(bn.weight, lambda o: o.copy_(dg))
-            _deliver_grad(bn.bias, lambda o: o.copy_(db))
-        return dg, db, finish_tmp
 
     def _deliver_bn_grads(self, bn, run) -> None:
         """``run(dgamma_out, dbeta_out)`` writes dγ, dβ; route them into the flat store."""
@@ -418,13 +317,11 @@ class FusedStages:
         independent work (a weight gradient) before ``_bn_bwd_finish``.  Single GPU: nothing
         to wait for (one fused launch in the finish)."""
         C = bn.num_features
-        if isinstance(partial, tuple) and partial[0] == "tail":
-            return ("done", bn, partial[1], None, bs)  # finalized by the dgrad's last blocks
         if not st.comm or st.ipc is not None:
             return ("local", bn, partial, nblk_seg, bs, st.ipc)
         dev = partial.device
         sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_reduce_fused(partial, abs(nblk_seg), S, C, 0, sums, zero_after=nblk_seg < 0)
+        ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, sums)
         scratch = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
         self._deliver_bn_grads(bn, lambda dg, db: ops.bn_bwd_finalize(
             sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db, scratch))
@@ -434,8 +331,6 @@ class FusedStages:
     def _bn_bwd_finish(self, ops, h, S: int) -> torch.Tensor:
         """Phase 2: coef [3][S][C] for the input gradient (from the global sums)."""
         bn, bs = h[1], h[4]
-        if h[0] == "done":
-            return h[2]
         C = bn.num_features
         dev = bs.mi.device
         coef = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
@@ -445,9 +340,8 @@ class FusedStages:
             partial, nblk_seg, ipc = h[2], h[3], h[5]
             kw = ipc.kwargs(site_key(bn, "bwd"), S, C) if ipc is not None else {}
             self._deliver_bn_grads(bn, lambda dg, db: ops.bn_reduce_fused(
-                partial, abs(nblk_seg), S, C, 2, None, bs.count, 0.0, 0.0, None, None, bs.mi,
-                None, bn.weight.detach(), None, None, dg, db, coef, **kw,
-                zero_after=nblk_seg < 0))
+                partial, nblk_seg, S, C, 2, None, bs.count, 0.0, 0.0, None, None, bs.mi,
+                None, bn.weight.detach(), None, None, dg, db, coef, **kw))
         else:
             sums, work = h[2], h[3]
             work.wait()
@@ -505,7 +399,7 @@ class FusedStages:
         M = dyn.numel() // dyn.shape[-1]
         return (getattr(self, "fused_bwd1x1", False) and cs.k == 1 and cs.stride == 1
                 and cs.conv.out_channels == 256 and cs.conv.in_channels == 64
-                and xin is a_prev and pro_ss is not None and self._groups() == 0
+                and xin is a_prev and pro_ss is not None
                 and M % S == 0 and (M // S) % 64 == 0 and M * 256 * 2 < (1 << 31))
 
     def _bwd1x1_fused(self, ops, dyn, bnb, cs: _ConvSpec, a_prev, bs_prev: _BNState, S: int):
@@ -554,10 +448,17 @@ class FusedStages:
         return (self.bnb_prologue and cs.k == 1 and cs.stride == 1 and M % S == 0
                 and (M // S) % 256 == 0 and cs.conv.in_channels <= getattr(self, "_bnb_max_cin", 128))
 
+    def _lazy_bn1_ok(self, b: _BlockSpec, a1: torch.Tensor, S: int) -> bool:
+        """BN1's backward applied in conv1's dgrad / weight-gradient operand prologues instead
+        of a materialising pass (a bottleneck's 1x1 stride-1 conv1)."""
+        cs0 = b.convs[0]
+        M = a1.numel() // a1.shape[-1]
+        return (getattr(self, "lazy_bn1", False) and cs0.k == 1 and cs0.stride == 1
+                and M % S == 0 and (M // S) % 256 == 0)
+
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
                dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,
-               bnb: Optional[Tuple] = None, tail_bn: Optional[Tuple] = None,
-               acc_keys: Optional[Tuple] = None, compact: bool = False,
+               bnb: Optional[Tuple] = None, compact: bool = False,
                sub_resid: bool = False):
         """dx (NHWC) = conv-transpose(dy).  ``accumulate``: dx += result (dx must be given).
 
@@ -572,11 +473,6 @@ class FusedStages:
                                           the partials of its downsample BN too → (p3, pd)
         ``bnb = (a, coef)`` (1x1 stride-1 only): the A operand is the BatchNorm backward
         coef.A·dyn + coef.B·a + coef.D computed in the prologue.
-        ``acc_keys = (key, key2)``: BatchNorm sites of the partials (and of the second stream)
-        for the atomic accumulators; blocks-per-segment is then returned negative (-G).
-        ``tail_bn = (bn, bn_state, st)``: when the partials come from ONE launch (stride 1, no
-        second BN stream) its last blocks also finalize that BatchNorm's backward — the
-        partials entry of the result is then ("tail", coef) with dγ, dβ already delivered.
         ``compact`` (stride-2 1x1, pad 0): return the dgrad only at the even input positions, as
         a dense [N, ceil(H/2), ceil(W/2), Ci] tensor (one stride-1 GEMM, no zero fill).
         ``sub_resid``: the residual (``dx`` with ``accumulate``, or bn_epi's resid) is such a
@@ -665,41 +561,11 @@ class FusedStages:
                              epi_tables=tables, bnb=bpro)
             chosen.append((wt, g, M, seg, ops.igemm_variant_bm(v), v))
         seg_blocks = sum(seg // bm for (_, _, _, seg, bm, _) in chosen)
-        G = self._groups() if acc_keys is not None else 0
-        use_tail = (tail_bn is not None and len(chosen) == 1 and self._tail_ok(tail_bn[2], Ci, S)
-                    and not (bn_epi[0] == "res" and bn_epi[5] is not None))
-        if G and not use_tail:  # atomic replica partials (see __init__)
-            partial = self._acc(acc_keys[0], S, G, Ci, dev)
-            second, partial2 = None, None
-            if bn_epi[0] == "res" and bn_epi[5] is not None:
-                partial2 = self._acc(acc_keys[1], S, G, Ci, dev)
-                second = (bn_epi[5], bn_epi[6], partial2)
-            base = 0
-            for wt, g, M, seg, bm, v in chosen:
-                igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
-                             epi_tables=tables, remap=(seg_blocks, base), second=second,
-                             bnb=bpro, stats_groups=G)
-                base += seg // bm
-            if partial2 is not None:
-                return dx, (partial, partial2), -G
-            return dx, partial, -G
         partial = torch.empty((S * seg_blocks * 2 * Ci,), device=dev, dtype=torch.float32)
         second, partial2 = None, None
         if bn_epi[0] == "res" and bn_epi[5] is not None:
             partial2 = torch.empty_like(partial)
             second = (bn_epi[5], bn_epi[6], partial2)
-        if (tail_bn is not None and len(chosen) == 1 and second is None
-                and self._tail_ok(tail_bn[2], Ci, S)):
-            bn, bs, st = tail_bn
-            wt, g, M, seg, bm, v = chosen[0]
-            coef = torch.empty((3 * S * Ci,), device=dev, dtype=torch.float32)
-            dg, db, finish = self._bn_grad_targets(bn)
-            tail = self._tail_spec(bn, 2, S, st, 0, bs.count, bs.mi, dgamma=dg, dbeta=db,
-                                   coef=coef)
-            igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
-                         epi_tables=tables, bnb=bpro, tail=tail)
-            finish()
-            return dx, ("tail", coef), seg_blocks
         base = 0
         for wt, g, M, seg, bm, v in chosen:
             igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
@@ -805,25 +671,24 @@ class FusedStages:
                 forked = True
             for ci_, cs in enumerate(b.convs):
                 _ext.TAG = f"{b.name} conv{ci_ + 1} fwd"
-                if pro_ss is not None and cs.k > 1 and not self._patch_pro_ok(cur, cs):
+                if pro_ss is not None and cs.k > 1:
                     # a k x k conv re-gathers every input pixel k² times: applying BN+ReLU in
-                    # its prologue costs more VALU work than one materialising pass (measured);
-                    # the LDS-resident patch kernels apply it once per patch pixel instead
+                    # its prologue costs more VALU work than one materialising pass (measured,
+                    # also for the LDS-resident patch kernels: r3 optimisation log)
                     bmat = torch.empty_like(cur)
                     ops.bn_apply_ss(cur, pro_ss, None, None, bmat, S, True)
                     cur, pro_ss = bmat, None
                 tp.ins.append((cur, pro_ss))
                 if ci_ == 0 and dual is not None:
-                    a, partial, nblk, bs = self._conv_fwd(ops, cur, cs, None, S, dual=dual, st=st)
+                    a, partial, nblk = self._conv_fwd(ops, cur, cs, None, S, dual=dual)
                     self.dual_launches += 1
                     if b.down is not None and br is not None:
                         fork_down()  # after the launch that writes its input x
                         forked = True
                 else:
-                    a, partial, nblk, bs = self._conv_fwd(ops, cur, cs, pro_ss, S, st=st)
-                if bs is None:
-                    rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
-                    bs = self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st)
+                    a, partial, nblk = self._conv_fwd(ops, cur, cs, pro_ss, S)
+                rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
+                bs = self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st)
                 tp.acts.append(a)
                 tp.bns.append(bs)
                 cur, pro_ss = a, bs.ss
@@ -863,12 +728,10 @@ class FusedStages:
         return self._branch
 
     def _down_fwd(self, ops, b: _BlockSpec, tp: _BlockTape, x, S: int, st, slot: int = 0):
-        ad, partial, nblk, bs = self._conv_fwd(ops, x, b.down, None, S, st=st, slot=slot)
+        ad, partial, nblk = self._conv_fwd(ops, x, b.down, None, S)
         tp.ad = ad
-        if bs is None:
-            rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
-            bs = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st, slot=slot)
-        tp.bnd = bs
+        rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
+        tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st, slot=slot)
 
     def backward(self, gout: torch.Tensor, tapes: List[_BlockTape]) -> torch.Tensor:
         ops = _ext.ops()
@@ -967,6 +830,7 @@ class FusedStages:
                 resid_f, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S, compact=compact)
         # conv chain, last to first: dgrad (+ BN-bwd partials) → start BN all-reduce → wgrad →
         # finish BN → apply
+        lazy0 = None
         for i in range(L, 0, -1):
             cs = b.convs[i]
             xin, pro_ss = tp.ins[i]
@@ -979,14 +843,16 @@ class FusedStages:
                 h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
             else:
                 gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,
-                                           bn_epi=("mask", a_prev, bs_prev), bnb=bnb,
-                                           tail_bn=(b.convs[i - 1].bn, bs_prev, st),
-                                           acc_keys=((id(b.convs[i - 1].bn), "bwd"), None))
+                                           bn_epi=("mask", a_prev, bs_prev), bnb=bnb)
                 h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
                 _ext.TAG = f"{b.name} conv{i + 1} wgrad"
                 self._wgrad(ops, dyn, xin, cs, pro_ss, S, bnb=bnb)
             _ext.TAG = f"{b.name} bn{i} bwd"
             coef = self._bn_bwd_finish(ops, h, S)
+            if i == 1 and prev is not None and self._lazy_bn1_ok(b, a_prev, S):
+                lazy0 = (a_prev, coef)  # da1 never materialised: conv1's operand prologues
+                da = gm
+                continue
             da_next = torch.empty_like(a_prev)
             ops.bn_bwd_apply(gm, None, a_prev, coef, S, False, da_next, None)
             da = da_next
@@ -1008,15 +874,12 @@ class FusedStages:
         else:
             pb, ptp = prev
             pds = pb.down is not None
-            dx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S,
+            dx, part, nb = self._dgrad(ops, da, cs0, tp.x.shape, S, bnb=lazy0,
                                        dx=resid if b.down is not None and not compact else None,
                                        sub_resid=compact,
                                        bn_epi=("res", resid, ptp.mask, ptp.acts[-1],
                                                ptp.bns[-1].mi, ptp.ad if pds else None,
-                                               ptp.bnd.mi if pds else None),
-                                       tail_bn=(pb.convs[-1].bn, ptp.bns[-1], st),
-                                       acc_keys=((id(pb.convs[-1].bn), "bwd"),
-                                                 (id(pb.down.bn), "bwd") if pds else None))
+                                               ptp.bnd.mi if pds else None))
             if pds:
                 p3, pd = part
                 h = (self._bn_bwd_start(ops, pb.convs[-1].bn, p3, nb, ptp.bns[-1], S, st),
@@ -1024,7 +887,7 @@ class FusedStages:
             else:
                 h = (self._bn_bwd_start(ops, pb.convs[-1].bn, part, nb, ptp.bns[-1], S, st), None)
         _ext.TAG = f"{b.name} conv1 wgrad"
-        self._wgrad(ops, da, tp.x, cs0, None, S)
+        self._wgrad(ops, da, tp.x, cs0, None, S, bnb=lazy0)
         if b.down is not None:
             _ext.TAG = f"{b.name} ds wgrad"
             self._wgrad(ops, dad, tp.x, b.down, None, S)

@@ -48,14 +48,15 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
         return hit
     cands = []
     for v in range(ops.igemm_nvariants()):
-        if v in _IG_SKIP:
-            continue
         bm = ops.igemm_variant_bm(v)
         if dual is not None:
             if not ops.igemm_dual_ok(v, geom):
                 continue
         elif not ops.igemm_variant_ok(v, geom, psc is not None, bnb is not None):
             continue  # e.g. LDS-DMA variants: C % 64 == 0, BN-apply prologue only on 1x1
+        if (bnb is not None and emode & 255 == 4 and ops.igemm_variant_glds(v)
+                and bm * ops.igemm_variant_bn(v) > 256 * 128):
+            continue  # BN-backward prologue + mode-4 epilogue: not instantiated at 256 x 256
         if want_stats and M % bm:
             continue
         if psc is not None and pseg % bm:
@@ -89,13 +90,9 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
                  seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None,
-                 bnb=None, dual=None, tail=None, stats_groups: int = 0) -> None:
+                 bnb=None, dual=None) -> None:
     """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip);
     ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue;
-    ``stats_groups = G > 0``: ``stats`` is a zeroed [S][G][2][N] accumulator the epilogue adds
-    its partials into with float atomics (replica = row-block index mod G, conv.hip);
-    ``tail = (mode, tensors, floats, ints)``: the BatchNorm that consumes ``stats`` is reduced and
-    finalized by this launch's last blocks (csrc/bn_tail.h; see FusedStages._tail_spec);
     ``dual = (res, rss, out, mask)``: block-output prologue — A is a block's pre-BN conv3
     activation, ``pro`` its BN scale/shift, ``res`` the residual (``rss`` its BN [2][S][C] table
     or None for identity); the conv consumes relu(bn(A) + res') and also writes it to ``out``
@@ -112,14 +109,8 @@ def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=N
     em = epi[4] if epi is not None and len(epi) > 4 else None
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     c2, mi2, st2 = second if second is not None else (None, None, None)
-    if tail is None:
-        ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-                  seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask,
-                  stats_groups)
-    else:  # ``tail = (mode, tensors, floats, ints)``: BatchNorm finalize in the last blocks
-        ops.igemm_t(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess,
-                    emi, seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout,
-                    pmask, tail[0], tail[1], tail[2], tail[3])
+    ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
+              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask)
 
 
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):
@@ -144,59 +135,6 @@ def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=N
     return (stats, M // bm) if stats is not None else None
 
 
-def _parse_variants(spec):
-    """"a-b,c" -> {a..b, c}; None / empty -> None."""
-    if not spec:
-        return None
-    out = set()
-    for part in spec.split(","):
-        lo, _, hi = part.partition("-")
-        out.update(range(int(lo), int(hi or lo) + 1))
-    return out
-
-
-# SIMCLR_IGEMM_SKIP="v,...": leave these conv tile variants out of the autotuner's candidates
-# (A/B experiments, e.g. 20 = the persistent layer1 3x3 kernel)
-_IG_SKIP = frozenset(int(v) for v in os.environ.get("SIMCLR_IGEMM_SKIP", "").split(",")
-                     if v.strip().isdigit())
-# The persistent layer1 3x3 kernel (variant 20) is opt-in (SIMCLR_IGEMM_PPATCH=1;
-# profiles/r3_optimization_log.md): bitwise-equal conv outputs, end to end neutral, but its
-# epilogue sums the BatchNorm partials in another order and the ResNet-50 batch-128 golden run
-# (tests/test_gpu_e2e.py) drifted past its bounds with it in 2 of 2 runs.  The single-stage
-# 2-blocks-per-CU short-K tiles (21, 22) are on (SIMCLR_IGEMM_SHORTK=0 leaves them out): 3-15 %
-# faster expansion / reduction 1x1 convs, golden run within bounds in 2 of 2 runs.
-if os.environ.get("SIMCLR_IGEMM_PPATCH", "0") != "1":
-    _IG_SKIP = _IG_SKIP | {20}
-# the single-stage 128 x 128 forward tile (23) and weight-gradient tiles (wgrad 20, 21): end to
-# end neutral, and with them in the candidate set the golden run drifted to 0.124 (bound 0.12):
-# opt-in (SIMCLR_TILES_EXTRA=1)
-_EXTRA = os.environ.get("SIMCLR_TILES_EXTRA", "0") == "1"
-if not _EXTRA:
-    _IG_SKIP = _IG_SKIP | {23}
-if os.environ.get("SIMCLR_IGEMM_SHORTK", "1") == "0":
-    _IG_SKIP = _IG_SKIP | {21, 22}
-# SIMCLR_WGRAD_VARIANTS="lo-hi,...": autotune the weight gradients over these variants only
-# (attribution experiments: register-staged vs LDS-DMA tiles beside the dgrad chain)
-_WG_ONLY = _parse_variants(os.environ.get("SIMCLR_WGRAD_VARIANTS", ""))
-# split reduction inside the weight-gradient kernel (last arriver per tile, conv.hip
-# wgrad_finish) instead of separate reduce launches.  Opt-in (SIMCLR_WGRAD_INKERNEL_REDUCE=1):
-# measured 25.06 vs 23.06 ms/step (tools/envab.sh, 2 rounds) — one block per output tile reads
-# ~13 x 64 KB of slabs with ~16 KB in flight, a latency-bound serial tail on every weight
-# gradient, where the separate reduce spreads the same bytes over the whole chip
-_WG_INKERNEL = os.environ.get("SIMCLR_WGRAD_INKERNEL_REDUCE", "0") == "1"
-# zeroed, self-resetting arrival tickets per (problem, variant, stream use): launches that share
-# a buffer are ordered on one stream (a site's weight gradients) — the tuning trials and the
-# live launch use separate buffers
-_TICKETS: dict = {}
-
-
-def _tickets(ops, key, geom, v, dev, trial: bool):
-    k = (key, v, trial, dev)
-    t = _TICKETS.get(k)
-    if t is None:
-        t = torch.zeros(ops.wgrad_tiles(geom, v), device=dev, dtype=torch.int32)
-        _TICKETS[k] = t
-    return t
 
 
 def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
@@ -224,17 +162,13 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
     def launch(v, o, trial=False):
         splits = nsplit(v)
         partial = torch.empty((splits * N * K,), device=dY.device, dtype=torch.float32)
-        tk = _tickets(ops, key, geom, v, dY.device, trial) if _WG_INKERNEL else None
         ops.wgrad(dY, X, partial, o, geom, splits, creal, 0.0, psc, psh, seg_rows, prelu, pS, v,
-                  dY2, dcoef, dseg, dS, tk)
+                  dY2, dcoef, dseg, dS)
 
     v = tuning.cached(key)
     if v is None:
         cands = [v for v in range(ops.wgrad_nvariants())
-                 if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)
-                 and (_EXTRA or v < 20)]
-        if _WG_ONLY is not None:  # experiment: restrict the candidates (fallback: all)
-            cands = [v for v in cands if v in _WG_ONLY] or cands
+                 if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)]
         v = tuning.pick(key, cands, 1 if N <= 64 else 0,
                         lambda vv: launch(vv, torch.empty_like(out), trial=True))
     launch(v, out)

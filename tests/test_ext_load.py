@@ -13,7 +13,7 @@ SO = ROOT / "simclr_amd" / "_C.so"
 @pytest.mark.skipif(not SO.exists(), reason="extension not built")
 def test_extension_loads_and_registers_ops():
     code = ("import torch; torch.ops.load_library(%r); o = torch.ops.simclr_amd; "
-            "names = ['igemm', 'igemm_t', 'wgrad', 'bn_reduce_fused', 'ipc_open', 'maxpool_fwd', "
+            "names = ['igemm', 'wgrad', 'bn_reduce_fused', 'ipc_open', 'maxpool_fwd', "
             "'ce_topk', 'class_sums', 'augment', 'lars_update', 'nt_forward']; "
             "[getattr(o, n).default for n in names]; print('ok')" % str(SO))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)

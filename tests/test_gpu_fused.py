@@ -189,8 +189,9 @@ def test_fused_stages_match_module_path(base, stem, batch, block_out, monkeypatc
     embeddings, so bf16 rounding alone moves some gradients by tens of percent: the check is
     relative to the module path's own distance from fp32, not an absolute tolerance.)"""
     from simclr_amd.loss.ntxent import NTXent
-    # block_out: every block output formed in the next conv1's prologue (SIMCLR_BLOCK_OUT_PROLOGUE)
-    monkeypatch.setenv("SIMCLR_BLOCK_OUT_PROLOGUE", "1" if block_out else "0")
+    # block_out: every block output formed in the next conv1's prologue
+    from simclr_amd.models.fused import FusedStages
+    monkeypatch.setattr(FusedStages, "BLOCK_OUT_PROLOGUE", bool(block_out))
     dev = torch.device(DEV, 0)
     torch.manual_seed(5)
     x = _bf(torch.rand(2 * batch, 8, 32, 32, device=dev)).contiguous(

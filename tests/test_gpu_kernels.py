@@ -424,90 +424,6 @@ def test_igemm_glds_variants(ops, k, s, p, C, Co, H):
             assert _rel(st, s0) < 1e-3, (v, mode)
 
 
-@pytest.mark.parametrize("N", [160, 8, 1024])
-def test_igemm_persistent_patch(ops, N):
-    """Persistent resident-weight 3x3 kernel (igemm_ppatch, variant 20; ResNet-50 layer1 conv2
-    and its dgrad) with several tiles per block (N=160: 640 tiles over at most one block per CU,
-    so the double-buffered patch, uneven runs and idle blocks are all exercised) against an fp32
-    torch conv (plain + BN statistics, BN-apply prologue) and the per-tile patch kernel (v15) for
-    the BN-backward epilogues (modes 3 / 4)."""
-    from simclr_amd.ops.conv_hip import fwd_geom
-    torch.manual_seed(N)
-    C = Co = 64
-    H = W = 32
-    S = 2
-    V = 20
-    x = _bf(torch.randn(N, C, H, W, device=DEV))
-    w = _bf(torch.randn(Co, C, 3, 3, device=DEV) / (C * 9) ** 0.5)
-    g = fwd_geom(N, H, W, C, H, W, 3, 3, 1, 1, Co)
-    assert ops.igemm_variant_ok(V, g, True, False) and ops.igemm_variant_bm(V) == 256
-    M = N * H * W
-    seg = M // S
-    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
-    wo = w.permute(0, 2, 3, 1).contiguous()
-    refn = F.conv2d(x.float(), w.float(), None, 1, 1).permute(0, 2, 3, 1)
-    out = torch.empty(N, H, W, Co, device=DEV, dtype=torch.bfloat16)
-    st = torch.empty((M // 256) * 2 * Co, device=DEV)
-    ops.igemm(xn, wo, out, None, st, g, None, None, 0, False, 0, None, None, V)
-    assert _rel(out, refn) < 1e-2
-    of = out.float().reshape(-1, Co)
-    s2 = st.view(M // 256, 2, Co).sum(0)
-    assert _rel(s2[0], of.sum(0)) < 1e-3 and _rel(s2[1], (of * of).sum(0)) < 1e-3
-    # BN-apply + ReLU prologue, per-segment tables
-    sc = (torch.rand(S, C, device=DEV) + 0.5).contiguous()
-    sh = (torch.randn(S, C, device=DEV) * 0.3).contiguous()
-    segi = torch.arange(N, device=DEV) // (N // S)
-    a = _bf(torch.relu(x.float() * sc[segi][:, :, None, None] + sh[segi][:, :, None, None]))
-    refa = F.conv2d(a.float(), w.float(), None, 1, 1).permute(0, 2, 3, 1)
-    ops.igemm(xn, wo, out, None, None, g, sc, sh, seg, True, 0, None, None, V)
-    assert _rel(out, refa) < 1e-2
-    # BN-backward epilogues against the per-tile patch kernel
-    yy = _bf(torch.randn(N, H, W, Co, device=DEV))
-    xa = _bf(torch.randn(N, H, W, Co, device=DEV))
-    r = _bf(torch.randn(N, H, W, Co, device=DEV))
-    mi = torch.cat([torch.randn(S, Co, device=DEV) * 0.2,
-                    torch.rand(S, Co, device=DEV) + 0.5]).reshape(-1).contiguous()
-    ss = torch.cat([torch.rand(S, Co, device=DEV) + 0.5,
-                    torch.randn(S, Co, device=DEV) * 0.3]).reshape(-1).contiguous()
-    for mode, ea, eb, ec in ((3, None, yy, None), (4, r, yy, xa)):
-        outs = []
-        for v in (V, 15):
-            o = torch.empty(N, H, W, Co, device=DEV, dtype=torch.bfloat16)
-            s_ = torch.empty((M // 256) * 2 * Co, device=DEV)
-            ops.igemm(xn, wo, o, None, s_, g, None, None, 0, False, mode, ea, eb, v, ss, mi, seg,
-                      0, 0, ec, None, None, None, None, None, None)
-            outs.append((o, s_.view(M // 256, 2, Co).sum(0)))
-        assert _rel(outs[0][0], outs[1][0]) < 1e-2, mode
-        assert _rel(outs[0][1], outs[1][1]) < 1e-3, mode
-
-
-def test_igemm_glds_dgrad_parity_classes(ops):
-    """Stride-2 dgrad parity-class geometry (negative tap step, strided output rows) on the
-    LDS-DMA kernel against the register-staged kernel, which the conv tests pin to torch."""
-    torch.manual_seed(5)
-    N, H, W, Ci, Co, KH = 4, 16, 16, 64, 128, 3
-    OH, OW, pad = 8, 8, 1
-    dyn = _bf(torch.randn(N, OH, OW, Co, device=DEV))
-    wo = _bf(torch.randn(Co, KH, KH, Ci, device=DEV) * 0.05)
-    for r in (0, 1):
-        for c in (0, 1):
-            kh0, kw0 = (r + pad) % 2, (c + pad) % 2
-            nkh, nkw = (KH - kh0 + 1) // 2, (KH - kw0 + 1) // 2
-            ohc, owc = (H - r + 1) // 2, (W - c + 1) // 2
-            wt = torch.empty((Ci, nkh, nkw, Co), device=DEV, dtype=torch.bfloat16)
-            ops.weight_transform(wo, wt, [Co, KH, KH, Ci, nkh, nkw, kh0, 2, kw0, 2])
-            g = [N, OH, OW, Co, ohc, owc, nkh, nkw, 1, 1, -1, -1, (r + pad - kh0) // 2,
-                 (c + pad - kw0) // 2, Ci, H, W, 2, 2, r, c, Ci]
-            vs = [v for v in _glds_variants(ops) if ops.igemm_variant_ok(v, g, False, False)]
-            outs = []
-            for v in [0] + vs:
-                o = torch.zeros(N, H, W, Ci, device=DEV, dtype=torch.bfloat16)
-                ops.igemm(dyn, wt, o, None, None, g, None, None, 0, False, 0, None, None, v)
-                outs.append(o)
-            for v, o in zip(vs, outs[1:]):
-                assert torch.equal(o, outs[0]) or _rel(o, outs[0]) < 1e-2, (r, c, v)
-
-
 @pytest.mark.parametrize("k,s,p,C,Co,H", [(1, 1, 0, 64, 256, 16), (3, 1, 1, 64, 64, 16),
                                            (3, 2, 1, 128, 192, 16), (1, 2, 0, 128, 128, 16),
                                            (3, 1, 1, 256, 512, 4), (3, 1, 1, 64, 64, 5),
@@ -539,48 +455,3 @@ def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
             out = torch.empty(Co, k, k, C, device=DEV)
             ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, None, None, 0, False, 1, v)
             assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)
-
-
-@pytest.mark.parametrize("k,s,p,C,Co,H", [(1, 1, 0, 64, 256, 16), (3, 1, 1, 64, 64, 16),
-                                           (3, 2, 1, 128, 192, 16), (3, 1, 1, 64, 64, 32),
-                                           (3, 1, 1, 256, 512, 4), (3, 1, 1, 64, 64, 5),
-                                           (1, 1, 0, 256, 64, 32)])
-def test_wgrad_inkernel_split_reduce_every_variant(ops, k, s, p, C, Co, H):
-    """In-launch split reduction (conv.hip wgrad_finish: last arriver per tile sums the slabs in
-    split order): every admissible variant and split counts 1 / 3 / default / 40 (> the
-    two-level threshold of the separate reduce) against torch's fp32 weight gradient and the
-    separate-reduce path; the self-resetting tickets are reused across launches."""
-    from simclr_amd.ops.conv_hip import fwd_geom
-    torch.manual_seed(17)
-    N = 8
-    x = _bf(torch.randn(N, C, H, H, device=DEV))
-    wr = (_bf(torch.randn(Co, C, k, k, device=DEV)) * 0.05).float().requires_grad_(True)
-    y = F.conv2d(x.float(), wr, None, s, p)
-    gy = _bf(torch.randn_like(y))
-    y.backward(gy.float())
-    OH, OW = y.shape[-2:]
-    g = fwd_geom(N, H, H, C, OH, OW, k, k, s, p, Co)
-    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
-    dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
-    K = k * k * C
-    M = N * OH * OW
-    vs = [v for v in range(ops.wgrad_nvariants()) if ops.wgrad_variant_ok(v, g, False, False)]
-    assert vs
-    for v in vs:
-        iters = M // 256 if v == 17 else (M + 63) // 64
-        tk = torch.zeros(ops.wgrad_tiles(g, v), device=DEV, dtype=torch.int32)
-        for splits in sorted({1, 3, ops.wgrad_splits(g, v), min(40, iters)}):
-            part = torch.empty(splits * Co * K, device=DEV)
-            a = torch.full((Co, k, k, C), float("nan"), device=DEV)
-            b = torch.empty(Co, k, k, C, device=DEV)
-            for _ in range(2):  # second launch: tickets were reset by the first
-                ops.wgrad(dyn, xn, part, a, g, splits, C, 0.0, None, None, 0, False, 1, v,
-                          None, None, 0, 1, tk)
-            ops.wgrad(dyn, xn, part, b, g, splits, C, 0.0, None, None, 0, False, 1, v)
-            assert int(tk.abs().sum()) == 0, (v, splits)
-            assert torch.isfinite(a).all(), (v, splits)
-            if splits <= 32:  # same slab_sum4 order as the one-level separate reduce: bitwise
-                assert torch.equal(a, b), (v, splits)
-            else:  # the separate reduce sums in groups of 16 first: fp32 reassociation only
-                assert _rel(a, b) < 1e-6, (v, splits, _rel(a, b))
-            assert _rel(a.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)

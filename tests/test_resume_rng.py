@@ -66,7 +66,7 @@ def test_resume_restores_each_ranks_own_rng(tmp_path):
     assert [open(f"{path}.{r}").read() for r in range(2)] == ["ok", "ok"]
 
 
-@pytest.mark.parametrize("knob",["SIMCLR_SKIP_WGRAD", "SIMCLR_EXPERIMENT_SKIP_BNRED"])
+@pytest.mark.parametrize("knob", ["SIMCLR_SKIP_WGRAD"])
 def test_training_refuses_attribution_knobs(monkeypatch, knob):
     from simclr_amd.train.pretrain import pretrain
     from simclr_amd.train.supervised import supervised

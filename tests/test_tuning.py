@@ -25,11 +25,3 @@ def test_pick_default_outside_candidates_falls_back_to_first():
 
 def test_rounds_default():
     assert tuning.ROUNDS >= 1
-
-
-def test_parse_variants():
-    assert conv_hip._parse_variants("") is None
-    assert conv_hip._parse_variants(None) is None
-    assert conv_hip._parse_variants("0-5,17") == {0, 1, 2, 3, 4, 5, 17}
-    assert conv_hip._parse_variants("6-17") == set(range(6, 18))
-    assert conv_hip._parse_variants("3") == {3}

@@ -2,7 +2,7 @@
 partial-array shapes of the ResNet-50 CIFAR step (batch 512x2): per-call time from a hipGraph
 of back-to-back launches (no launch overhead), per (C, blocks-per-segment).
 
-Usage (GPU box): SIMCLR_BNRED_ROWS=16 SIMCLR_BNRED_CAP=64 python tools/bench_reduce.py"""
+Usage (GPU box): python tools/bench_reduce.py"""
 import os
 import sys
 
@@ -19,7 +19,7 @@ def main():
     _ext.require()
     ops = torch.ops.simclr_amd
     S, reps = 2, 50
-    print(f"rows={os.environ.get('SIMCLR_BNRED_ROWS', 16)} cap={os.environ.get('SIMCLR_BNRED_CAP', 64)}")
+
     for C, nblk in SHAPES:
         part = torch.randn(S * nblk * 2 * C, device="cuda")
         mi = torch.empty(2 * S * C, device="cuda")
