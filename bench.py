@@ -206,12 +206,7 @@ def run_ours(args, rank, world, dev):
         args.mode_probe_ms = [round(float(v) / 3 * 1000.0, 3) for v in tt.tolist()]
     args.graph = tr.graph is not None
     loss = None
-    import contextlib
-    ctx = contextlib.nullcontext()
-    if os.environ.get("SIMCLR_HP_STREAM") == "1" and dev.type == "cuda" and not args.graph:
-        # experiment: the step's main stream at the highest priority (side streams stay low)
-        lo, hi = torch.cuda.Stream.priority_range()
-        ctx = torch.cuda.stream(torch.cuda.Stream(device=dev, priority=hi))
+
     def measure():
         nonlocal loss
         for _ in range(args.warmup):
@@ -235,18 +230,17 @@ def run_ours(args, rank, world, dev):
         args.host_issue_ms = host / args.steps * 1000.0
         return t0, t1
 
-    with ctx:
+    t0, t1 = measure()
+    if ipc_guard():
+        # an IPC spin timed out inside the timed region: those steps ran on partial BatchNorm
+        # statistics, so the measurement is void — every rank is on RCCL now (collective
+        # decision) and the K steps are timed again
+        print(f"[bench] rank {rank}: IPC statistics exchange timed out in the timed region; "
+              "re-timing on RCCL", file=sys.stderr, flush=True)
+        tr.graph = None
+        args.graph = False
+        args.bn_comm = "rccl(ipc-timeout, re-timed)"
         t0, t1 = measure()
-        if ipc_guard():
-            # an IPC spin timed out inside the timed region: those steps ran on partial
-            # BatchNorm statistics, so the measurement is void — every rank is on RCCL now
-            # (collective decision) and the K steps are timed again
-            print(f"[bench] rank {rank}: IPC statistics exchange timed out in the timed region; "
-                  "re-timing on RCCL", file=sys.stderr, flush=True)
-            tr.graph = None
-            args.graph = False
-            args.bn_comm = "rccl(ipc-timeout, re-timed)"
-            t0, t1 = measure()
 
     return t1 - t0, float(loss.item()) if loss is not None else float("nan")
 

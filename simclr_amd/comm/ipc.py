@@ -35,7 +35,9 @@ import torch.distributed as dist
 from ..ops import _ext
 from ..parallel.state import site_key, tag_sites  # noqa: F401
 
-DEFAULT_WORDS = 1 << 23  # 64 MiB arena: ResNet-50 fwd + bwd sites at W = 8 need ~30 MiB
+# 128 MiB arena: ResNet-50 fwd + bwd BatchNorm sites at W = 8 need ~30 MiB, the gathered
+# NT-Xent's embedding all-gather and column-gradient reduce-scatter ~24 MiB more
+DEFAULT_WORDS = 1 << 24
 MAX_WORLD = 16
 
 
@@ -74,6 +76,21 @@ class SiteTable:
         self.next_epoch += ne
         return rec[:3]
 
+    def get_raw(self, key, words: int, nepochs: int) -> Tuple[int, int, int]:
+        """A region of ``words`` words and ``nepochs`` epoch counters (the IPC collectives)."""
+        key = ("raw", key, words, nepochs)
+        if key in self.sites:
+            off, eo, ne, _ = self.sites[key]
+            return off, eo, ne
+        if self.next_word + words > self.words or self.next_epoch + nepochs > self.epochs:
+            raise RuntimeError("IPC arena exhausted "
+                               f"({self.next_word + words} > {self.words} words)")
+        rec = (self.next_word, self.next_epoch, nepochs, words)
+        self.sites[key] = rec
+        self.next_word += words
+        self.next_epoch += nepochs
+        return rec[:3]
+
 
 class IpcStatsExchange:
     def __init__(self, rank: int, world: int, device: torch.device, group=None,
@@ -106,6 +123,25 @@ class IpcStatsExchange:
         return dict(ipc_peers=self.peers, ipc_arena=self.arena, ipc_site=off,
                     ipc_epoch=self.epoch[eo:eo + ne], ipc_err=self.err, world=self.world,
                     rank=self.rank)
+
+    def _collective(self, op: int, key, src: torch.Tensor, dst: torch.Tensor, n: int) -> None:
+        ops = _ext.ops()
+        nb = int(ops.ipc_coll_blocks())
+        off, eo, ne = self.table.get_raw(key, 2 * self.world * n, nb)
+        ops.ipc_collective(op, src, dst, self.peers, self.arena, off, self.epoch[eo:eo + ne],
+                           self.err, self.world, self.rank)
+
+    def all_gather(self, key, src: torch.Tensor, dst: torch.Tensor) -> None:
+        """``dst`` ([W * len(src)], rank-major) = every rank's ``src`` — one kernel on the current
+        stream, one-shot stores into every peer's arena (csrc/comm.hip).  Same contract as
+        ``dist.all_gather_into_tensor``; ``key`` names the arena site (identical on all ranks)."""
+        self._collective(0, key, src, dst, src.numel() * src.element_size() // 4)
+
+    def reduce_scatter(self, key, src: torch.Tensor, dst: torch.Tensor) -> None:
+        """``dst`` = Σ_r (rank r's ``src``)[rank-th slice], fp32, summed in rank order (the same
+        bits on every rank).  Same contract as ``dist.reduce_scatter_tensor``."""
+        assert src.dtype == torch.float32 and dst.dtype == torch.float32
+        self._collective(1, key, src, dst, dst.numel())
 
     def failed(self) -> bool:
         """A spin timed out (a peer never delivered): the statistics of that step are wrong."""

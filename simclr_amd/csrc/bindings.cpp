@@ -568,6 +568,41 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
   bn_reduce_fused(q, cur_stream());
 }
 
+// one-shot IPC all-gather (op 0: dst [W][n] <- every rank's src [n]) or reduce-scatter (op 1:
+// dst [n] <- sum over ranks of src [W][n] row `rank`) of 32-bit words (comm.hip)
+void ipc_collective_op(int64_t op, const Tensor& src, const Tensor& dst, const Tensor& peers,
+                       const Tensor& arena, int64_t site, const Tensor& epoch, const Tensor& err,
+                       int64_t world, int64_t rank) {
+  TORCH_CHECK(op == 0 || op == 1, "ipc_collective: op 0 (all-gather) or 1 (reduce-scatter)");
+  const bool words = src.element_size() == 4 && dst.element_size() == 4;
+  const bool pairs = op == 0 && src.element_size() == 2 && dst.element_size() == 2;
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.is_contiguous() && dst.is_contiguous() &&
+                  (words || pairs),
+              "ipc_collective: contiguous 32-bit (or bf16 pairs for the all-gather) GPU tensors");
+  const int64_t nbytes = src.numel() * src.element_size();
+  TORCH_CHECK(nbytes % 4 == 0, "ipc_collective: payload must be whole 32-bit words");
+  const int64_t n = op == 0 ? nbytes / 4 : nbytes / 4 / world;
+  TORCH_CHECK(world >= 1 && world <= 16 && rank >= 0 && rank < world, "ipc_collective: world");
+  TORCH_CHECK(dst.numel() * dst.element_size() == (op == 0 ? world * n * 4 : n * 4),
+              "ipc_collective: dst size");
+  TORCH_CHECK(op == 0 || src.numel() * src.element_size() == world * n * 4,
+              "ipc_collective: reduce-scatter src must be [world][n] words");
+  check_dev(peers, at::kLong, "ipc_peers");
+  check_dev(arena, at::kLong, "ipc_arena");
+  check_dev(epoch, at::kInt, "ipc_epoch");
+  check_dev(err, at::kInt, "ipc_err");
+  TORCH_CHECK(peers.numel() == world, "ipc_collective: peer table size");
+  TORCH_CHECK(epoch.numel() >= IPC_COLL_BLOCKS, "ipc_collective: epoch counters");
+  TORCH_CHECK(site >= 0 && site + ipc_coll_region_words((int)world, (int)n) <= arena.numel(),
+              "ipc_collective: site outside the arena");
+  ipc_collective((int)op, static_cast<const uint32_t*>(src.data_ptr()),
+                 static_cast<uint32_t*>(dst.data_ptr()), (int)n,
+                 reinterpret_cast<uint64_t* const*>(peers.data_ptr<int64_t>()),
+                 reinterpret_cast<uint64_t*>(arena.data_ptr<int64_t>()), site,
+                 reinterpret_cast<unsigned*>(epoch.data_ptr<int>()), err.data_ptr<int>(),
+                 (int)world, (int)rank, cur_stream());
+}
+
 void bn_apply_ss_op(const Tensor& x, const Tensor& ss, const c10::optional<Tensor>& res,
                     const c10::optional<Tensor>& rss, const Tensor& y, int64_t S, bool relu,
                     const c10::optional<Tensor>& mask) {
@@ -910,6 +945,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("bn_stats(Tensor x, int S, Tensor(a!) partial) -> ()", &bn_stats);
   m.def("bn_reduce(Tensor partial, int nblk, int S, int C, Tensor(a!) stats) -> ()", &bn_reduce);
   m.def("bn_finalize(Tensor stats, int S, int C, float count, float eps, float momentum, Tensor(a!)? rm, Tensor(b!)? rv, Tensor(c!) mi, Tensor(d!)? nbt, Tensor? gamma=None, Tensor? beta=None, Tensor(e!)? ss=None) -> ()", &bn_final);
+  m.def("ipc_collective(int op, Tensor src, Tensor(a!) dst, Tensor peers, Tensor(b!) arena, int site, Tensor(c!) epoch, Tensor(d!) err, int world, int rank) -> ()", &ipc_collective_op);
+  m.def("ipc_coll_blocks() -> int", []() -> int64_t { return IPC_COLL_BLOCKS; });
   m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0) -> ()", &bn_reduce_fused_op);
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);

@@ -142,6 +142,15 @@ void bn_reduce_fused(const BnReduceFusedParams& q, hipStream_t s);
 inline long long bn_ipc_region_words(int world, int S, int C) {
   return 2LL * world * 2 * S * C;
 }
+
+// ---- comm.hip: one-shot IPC all-gather (op 0) / reduce-scatter (op 1) of 32-bit words over the
+// peer-mapped arenas (LL words; site = 2 parities x world x n words, IPC_COLL_BLOCKS epoch
+// counters)
+constexpr int IPC_COLL_BLOCKS = 64;
+long long ipc_coll_region_words(int world, int n);
+void ipc_collective(int op, const uint32_t* src, uint32_t* dst, int n, uint64_t* const* peers,
+                    uint64_t* own, long long site, unsigned* epoch, int* err, int world,
+                    int rank, hipStream_t s);
 // y = relu?(x*sc + sh + [res | res*rsc + rsh]); ss / rss are [2][S][C] scale/shift tables
 // optional mask: uint8 [R][C/8], bit e of byte (r, c/8) = (y[r][c] > 0)
 void bn_apply_ss(const uint16_t* x, const float* ss, const uint16_t* res, const float* rss,

@@ -92,7 +92,11 @@ class _NTXentHipFn(torch.autograd.Function):
             side.wait_stream(cur)
             zb_all = torch.empty((Ccols, D), device=dev, dtype=torch.bfloat16)
             with torch.cuda.stream(side):
-                dist.all_gather_into_tensor(zb_all, zb, group=st.group)
+                ipc = getattr(st, "ipc", None)
+                if ipc is not None:  # one-shot stores over xGMI (comm/ipc.py, csrc/comm.hip)
+                    ipc.all_gather(("ntxent", "z"), zb, zb_all)
+                else:
+                    dist.all_gather_into_tensor(zb_all, zb, group=st.group)
             zall = torch.empty((Ccols, D), device=dev, dtype=torch.float32)
             inv_all = torch.empty((Ccols,), device=dev, dtype=torch.float32)
             zn = zall[col_offset:col_offset + R]
@@ -162,7 +166,11 @@ class _NTXentHipFn(torch.autograd.Function):
             side.wait_stream(cur)
             mine = torch.empty((R, D), device=dev, dtype=torch.float32)
             with torch.cuda.stream(side):
-                dist.reduce_scatter_tensor(mine, d_cols, group=st.group)
+                ipc = getattr(st, "ipc", None)
+                if ipc is not None:
+                    ipc.reduce_scatter(("ntxent", "dcols"), d_cols, mine)
+                else:
+                    dist.reduce_scatter_tensor(mine, d_cols, group=st.group)
             # (d_cols / mine stay referenced until the join below, which orders every later
             # allocation on this stream after the side stream's use)
         s_row = ops.nt_bwd_splits(R, Ccols)

@@ -114,7 +114,8 @@ def test_golden_trajectory_resnet50_batch128_60_steps():
     """The flagship model trains on the bf16 HIP path: ResNet-50 (CIFAR stem), batch 128, 60
     optimizer steps (warmup + cosine, LARS) against the fp32 reference-semantics torch path
     from identical weights and views.  Both losses must fall by >= 0.3 (measured: 5.54 -> 4.8
-    on both paths) and the trajectories must agree (bounds below)."""
+    on both paths) and the trajectories must agree (bounds below) — with the autotuner ON, i.e.
+    the tile variants production selects, not a pinned default set."""
     from simclr_amd.data.datasets import synthetic_dataset
     from simclr_amd.data.loader import ContrastiveLoader
     from simclr_amd.config import compose, task_config, CONF_DIR
@@ -144,16 +145,14 @@ def test_golden_trajectory_resnet50_batch128_60_steps():
     assert t_hip.hip and not t_ref.hip
     with torch.no_grad():
         t_ref.store.master.copy_(t_hip.store.master)
-    # fixed tile variants (autotuner off, as under runtime.deterministic): the 60-step trajectory
-    # is sensitive to the fp32 summation order of whichever tiles win the timing near-ties on a
-    # given box (profiles/r3_optimization_log.md); pinned, the HIP side is the same on every box
-    from simclr_amd.ops import tuning
-    was = tuning.ENABLED
-    tuning.set_enabled(False)
-    try:
-        l_hip = [float(t_hip.step(x).item()) for x in xs]
-    finally:
-        tuning.set_enabled(was)
+    # the PRODUCTION path: autotuner on (the tiles training and bench.py select on this box).
+    # The fp32 reference runs stock MIOpen convolutions whose algorithm choice also varies from
+    # box to box, and the bf16-vs-fp32 rounding difference grows chaotically over the steps, so
+    # step-wise agreement is only demanded while the weights are still nearly identical (first
+    # 5 steps); afterwards the trajectories are compared as 10-step running means (the
+    # per-batch losses jump ±0.1).  Calibration (MI355X, 6 runs, pinned and autotuned tiles):
+    # first-5 max |d| <= 0.013; 10-step running-mean |d| max 0.033-0.153, mean 0.012-0.061.
+    l_hip = [float(t_hip.step(x).item()) for x in xs]
     l_ref = [float(t_ref.step(x).item()) for x in xs]
     diffs = [abs(a - b) for a, b in zip(l_hip, l_ref)]
     print("hip", [round(v, 3) for v in l_hip])
@@ -162,10 +161,7 @@ def test_golden_trajectory_resnet50_batch128_60_steps():
     first_h, last_h = sum(l_hip[:10]) / 10, sum(l_hip[-10:]) / 10
     first_r, last_r = sum(l_ref[:10]) / 10, sum(l_ref[-10:]) / 10
     assert last_h < first_h - 0.3 and last_r < first_r - 0.3, (first_h, last_h, first_r, last_r)
-    # step-wise agreement while the two weight trajectories are still close (measured on MI355X:
-    # max 0.035, mean 0.014 over the first 20 steps); afterwards bf16 vs fp32 rounding makes the
-    # per-batch losses (which jump ±0.1 from batch to batch) drift apart, so the later steps are
-    # compared as 5-step running means (measured max 0.081, mean 0.032 over 60 steps)
-    assert max(diffs[:20]) < 0.06 and sum(diffs[:20]) / 20 < 0.025, diffs[:20]
-    sm = [abs(sum(l_hip[i:i + 5]) - sum(l_ref[i:i + 5])) / 5 for i in range(len(xs) - 4)]
-    assert max(sm) < 0.12 and sum(sm) / len(sm) < 0.05, sm
+    assert max(diffs[:5]) < 0.04, diffs[:5]
+    rm = [abs(sum(l_hip[i:i + 10]) - sum(l_ref[i:i + 10])) / 10 for i in range(len(xs) - 9)]
+    print("10-step running-mean |d| max", max(rm), "mean", sum(rm) / len(rm))
+    assert max(rm) < 0.2 and sum(rm) / len(rm) < 0.08, rm

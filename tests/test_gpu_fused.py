@@ -197,9 +197,25 @@ def test_fused_stages_match_module_path(base, stem, batch, block_out, monkeypatc
     x = _bf(torch.rand(2 * batch, 8, 32, 32, device=dev)).contiguous(
         memory_format=torch.channels_last)
     res = {}
+    stages = {}  # mode -> {stage name: output activation (fp32, NCHW)}
+    orig_fwd = FusedStages.forward
+
+    def rec_fwd(self, xn):  # the fused executor's block outputs, per stage (last block wins)
+        out, tapes = orig_fwd(self, xn)
+        for b, tp in zip(self.blocks, tapes):
+            stages["fused"][b.name.split(".")[0]] = tp.out.float().permute(0, 3, 1, 2).clone()
+        return out, tapes
+    monkeypatch.setattr(FusedStages, "forward", rec_fwd)
     for mode in ("module", "fused", "fp32"):
         m2, store2 = _model(base, stem, dev)
         m2.f.use_fused_stages = mode == "fused"
+        stages[mode] = {}
+        hooks = []
+        if mode != "fused":
+            for ln in ("layer1", "layer2", "layer3", "layer4"):
+                hooks.append(getattr(m2.f, ln)[-1].register_forward_hook(
+                    lambda mod, inp, out, ln=ln, mode=mode:
+                    stages[mode].__setitem__(ln, out.detach().float().clone())))
         if mode == "fp32":
             with torch.no_grad():  # same (bf16-representable) weights, fp32 compute
                 store2.master.copy_(store2.shadow.float())
@@ -221,11 +237,24 @@ def test_fused_stages_match_module_path(base, stem, batch, block_out, monkeypatc
                     (ex.dual_launches, ex.out_apply_calls)
             else:
                 assert (ex.dual_launches, ex.out_apply_calls) == (0, nblk)
+        for h in hooks:
+            h.remove()
         res[mode] = (float(loss.detach()), store2.grad.clone(),
                      [(n, b.float().clone()) for n, b in m2.named_buffers() if "running" in n])
     lm, gm, bm = res["module"]
     lf, gf, bf = res["fused"]
     lr, gr, br = res["fp32"]
+    # per-stage relative error of the stage outputs vs fp32 (diagnostic dump: which stage moves
+    # the fused path's loss further from fp32 than the module path's), and a bound per stage
+    errs = {}
+    for ln in ("layer1", "layer2", "layer3", "layer4"):
+        w = stages["fp32"][ln]
+        errs[ln] = tuple((stages[m][ln] - w).norm().item() / (w.norm().item() + 1e-6)
+                         for m in ("fused", "module"))
+    print("STAGE-ERR fused/module vs fp32:",
+          {k: (round(a, 5), round(b, 5)) for k, (a, b) in errs.items()}, "loss", (lf, lm, lr))
+    for ln, (ef, em) in errs.items():
+        assert ef <= 1.5 * em + 5e-3, (ln, ef, em)
     # the loss at init is a softmax over nearly identical embeddings: bf16 paths move it by a
     # few 1e-2 depending on accumulation order (tile variants are autotuned per run)
     assert abs(lf - lr) <= 1.5 * abs(lm - lr) + 3e-2, (lm, lf, lr)
