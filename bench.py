@@ -37,6 +37,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "pretrain images/sec (whole node) + CIFAR-10 linear-probe top-1, ResNet-50"
 PG_TIMEOUT_S = float(os.environ.get("SIMCLR_BENCH_PG_TIMEOUT", "300"))
+PROBE_ROUNDS = 3  # execution-mode probe: 3 x (2 eager + 2 graph) interleaved steps
 
 
 def _free_port() -> int:
@@ -184,7 +185,7 @@ def run_ours(args, rank, world, dev):
         timed(2)  # eager warm-up: autotuning, allocator, communicators
         if ipc_guard():
             timed(1)
-        t_eager = timed(3)
+        t_eager = 0.0  # measured below, interleaved with the graph replays
     if args.graph and tr.hip:
         try:
             tr.capture(next_batch())
@@ -197,13 +198,21 @@ def run_ours(args, rank, world, dev):
         # execution-mode autotune: replaying the captured step vs issuing it eagerly (the HIP
         # graph executor loses part of the side-stream overlap — 24.0 vs 23.4 ms/step at N=1 —
         # while eager issue costs host time that grows with the ranks sharing the CPUs)
-        t_graph = timed(3)
+        # PROBE_ROUNDS interleaved rounds of 2 eager + 2 replayed steps (box drift hits both
+        # arms alike); the slower rank decides, the same choice on every rank
+        g, t_graph = tr.graph, 0.0
+        for _ in range(PROBE_ROUNDS):
+            tr.graph = None
+            t_eager += timed(2)
+            tr.graph = g
+            t_graph += timed(2)
+        n = 2 * PROBE_ROUNDS
         tt = torch.tensor([t_eager, t_graph], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         if float(tt[1]) >= float(tt[0]):
             tr.graph = None
-        args.mode_probe_ms = [round(float(v) / 3 * 1000.0, 3) for v in tt.tolist()]
+        args.mode_probe_ms = [round(float(v) / n * 1000.0, 3) for v in tt.tolist()]
     args.graph = tr.graph is not None
     loss = None
 

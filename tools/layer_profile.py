@@ -31,13 +31,18 @@ class _Timed:
             r = f(*args, **kw)
             e.record()
             from simclr_amd.ops import _ext as ext
-            lab, fl = _label(name, args)
-            self._log.append(((lab, fl, ext.TAG), s, e))
+            lab, fl, by = _label(name, args)
+            self._log.append(((lab, fl, by, ext.TAG), s, e))
             return r
         return wrap
 
 
+def _nb(t):
+    return t.numel() * t.element_size() if isinstance(t, torch.Tensor) else 0
+
+
 def _label(name, args):
+    """(label, flops, compulsory bytes): every operand read or written once (HBM roofline)."""
     if name == "igemm":
         g = args[5]
         M = g[0] * g[4] * g[5]
@@ -45,14 +50,28 @@ def _label(name, args):
         mode = args[10] if len(args) > 10 else 0
         pro = args[6] is not None
         kind = "fwd" if g[10] == 1 and g[12] <= 0 and g[17] == 1 else "dgrad"
-        return f"igemm {kind} M={M} N={g[14]} K={K} k={g[6]} s={g[8]}{' pro' if pro else ''} epi{mode}", 2.0 * M * g[14] * K
+        extra = [args[i] for i in (11, 12, 19, 20, 21, 25, 27, 28) if len(args) > i]
+        byts = _nb(args[0]) + _nb(args[1]) + 2 * M * g[14] + sum(_nb(t) for t in extra)
+        fus = (" bnb" if len(args) > 24 and args[24] is not None else "") + \
+              (" dual" if len(args) > 27 and args[27] is not None else "")
+        return (f"igemm {kind} M={M} N={g[14]} K={K} k={g[6]} s={g[8]}{' pro' if pro else ''}"
+                f"{fus} epi{mode & 255}", 2.0 * M * g[14] * K, byts)
     if name == "wgrad":
         g = args[4]
         M = g[0] * g[4] * g[5]
         K = g[6] * g[7] * g[3]
-        return f"wgrad M={M} N={g[14]} K={K} k={g[6]}{' pro' if args[8] is not None else ''}", 2.0 * M * g[14] * K
+        splits = args[5]
+        byts = _nb(args[0]) + _nb(args[1]) + 2 * 4 * splits * g[14] * K + _nb(args[3])
+        if len(args) > 14:
+            byts += _nb(args[14])
+        return (f"wgrad M={M} N={g[14]} K={K} k={g[6]}{' pro' if args[8] is not None else ''}",
+                2.0 * M * g[14] * K, byts)
     shape = tuple(args[0].shape) if hasattr(args[0], "shape") else ""
-    return f"{name} {shape}", 0.0
+    return f"{name} {shape}", 0.0, sum(_nb(t) for t in args)
+
+
+PEAK_FLOPS = 2.5e15   # bf16 dense MFMA peak (no sparsity)
+PEAK_BYTES = 6.3e12   # achievable HBM3E stream bandwidth (MI355X_MICROARCH.md: float4 copy)
 
 
 def main():
@@ -86,14 +105,20 @@ def main():
     for _ in range(a.steps):
         tr.step(next(it)[0])
     torch.cuda.synchronize()
-    agg = defaultdict(lambda: [0, 0.0, 0.0])
+    agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0])
     by_tag = defaultdict(float)
-    for (lab, flops, tag), s, e in log:
+    fam = defaultdict(lambda: [0.0, 0.0])  # kernel family -> [us, ideal us]
+    for (lab, flops, byts, tag), s, e in log:
         v = agg[lab]
         v[0] += 1
         t = s.elapsed_time(e) * 1e3
         v[1] += t
         v[2] += flops
+        v[3] += byts
+        ideal = max(flops / PEAK_FLOPS, byts / PEAK_BYTES) * 1e6
+        f = fam[lab.split(" ")[0] + (" " + lab.split(" ")[1] if lab.startswith("igemm") else "")]
+        f[0] += t
+        f[1] += ideal
         # aggregate blocks of the same stage: "layer1.2 conv3 dgrad" -> "layer1 conv3 dgrad"
         parts = tag.split(" ")
         if parts and parts[0].startswith("layer"):
@@ -102,10 +127,22 @@ def main():
     tot = sum(v[1] for v in agg.values()) / a.steps
     print(f"# per-op time, ResNet-50 CIFAR, batch {a.batch}x2 views, avg of {a.steps} steps\n")
     print(f"total timed op time/step: {tot / 1e3:.2f} ms\n")
-    print("| op | calls/step | us/step | % | TF/s |\n|---|---:|---:|---:|---:|")
-    for lab, (n, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        tf = f"{fl / (t * 1e-6) / 1e12:.0f}" if fl else ""
-        print(f"| {lab} | {n / a.steps:.1f} | {t / a.steps:.1f} | {100 * t / a.steps / tot:.1f} | {tf} |")
+    print("roofline per op: max(FLOP / 2.5 PF/s bf16 dense, compulsory bytes / 6.3 TB/s); "
+          "% = roofline time / measured time; bound = which term dominates\n")
+    print("| op | calls/step | us/step | % of step | TF/s | TB/s | bound | % roofline |\n"
+          "|---|---:|---:|---:|---:|---:|---|---:|")
+    for lab, (n, t, fl, by) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        sec = t * 1e-6
+        tf = f"{fl / sec / 1e12:.0f}" if fl else ""
+        tb = f"{by / sec / 1e12:.2f}"
+        ideal = max(fl / PEAK_FLOPS, by / PEAK_BYTES)
+        bound = "MFMA" if fl / PEAK_FLOPS > by / PEAK_BYTES else "HBM"
+        print(f"| {lab} | {n / a.steps:.1f} | {t / a.steps:.1f} | {100 * t / a.steps / tot:.1f} "
+              f"| {tf} | {tb} | {bound} | {100 * ideal / sec:.0f} |")
+    print("\n## by kernel family\n")
+    print("| family | us/step | roofline us/step | % roofline |\n|---|---:|---:|---:|")
+    for k, (t, ideal) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
+        print(f"| {k} | {t / a.steps:.1f} | {ideal / a.steps:.1f} | {100 * ideal / t:.0f} |")
     from simclr_amd.ops import tuning
     print("\n## autotuned tile variants (key -> variant)\n")
     ops = real
