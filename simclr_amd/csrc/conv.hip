@@ -2751,15 +2751,8 @@ int wgrad_splits(const ConvGeom& g, int variant) {
     const int v = e ? atoi(e) : 80;  // end of round 3: 80 beat 60 in 5 of 5 A/B rounds
     return v > 0 ? v : 100;
   }();
-  // SIMCLR_WGRAD_TARGET_PCT_BIG: the same for the 32x32-resolution weight gradients (layer1 /
-  // stem, >= 2^20 rows), the last ones of the backward, which overlap nothing at its tail
-  static const int pct_big = [] {
-    const char* e = getenv("SIMCLR_WGRAD_TARGET_PCT_BIG");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : pct;
-  }();
   const int target =
-      std::max(1, WG_VARIANTS[variant][2] * (M >= (1 << 20) ? pct_big : pct) / 100);
+      std::max(1, WG_VARIANTS[variant][2] * pct / 100);
   int splits = (target + tiles - 1) / tiles;
   int max_splits = patch ? iters : iters / 8;
   if (max_splits < 1) max_splits = 1;
