@@ -1154,18 +1154,77 @@ struct WgradArgs {
   int dp_seg_rows, dp_S;
 };
 
+// Weight-gradient MFMA shape: 16 = v_mfma_f32_16x16x32_bf16 (f32x4 accumulators), 32 =
+// v_mfma_f32_32x32x16_bf16 (f32x16).  Same FLOPs and LDS fragment bytes per wave tile; the
+// 32x32 form issues half the MFMA instructions and reads its operands as 32-column blocks.
+template <int MF> struct WMfma;
+template <> struct WMfma<16> { typedef f32x4 acc_t; };
+template <> struct WMfma<32> { typedef f32x16 acc_t; };
+
+// LDS swizzle of the weight-gradient operand images (XOR of 4-element units, 16-byte chunks kept
+// whole).  MF 16: tr_swz (the transposed half-wave read covers rows q, q + 8 x 16 columns).
+// MF 32: the half-wave read covers rows q = 0..3 x 32 columns (8 units = 16 banks): XOR the unit
+// by (r & 3) << 3 so the four rows land on disjoint 16-bank quarters (rows of 128 / 256
+// elements all start at bank 0).
+template <int W, int MF>
+__device__ __forceinline__ int wg_swz(int r, int col) {
+  if constexpr (MF == 16) {
+    return tr_swz<W>(r, col);
+  } else {
+    static_assert(W >= 128, "32x32 weight-gradient images need >= 32 units per row");
+    return ((((col >> 2) ^ ((r & 3) << 3))) << 2) | (col & 3);
+  }
+}
+
 // One 64-deep step of the weight-gradient tile from swizzled row-major LDS images (rows = m):
 // both MFMA operands are read transposed with ds_read_b64_tr_b16.
-template <int BCO, int BKK, int WM, int WN, int KS = 2>
-__device__ __forceinline__ void wgrad_mma(const uint16_t* Db, const uint16_t* Xb,
-                                          f32x4 (&acc)[BCO / WM / 16][BKK / WN / 16]) {
+template <int BCO, int BKK, int WM, int WN, int KS = 2, int MF = 16>
+__device__ __forceinline__ void wgrad_mma(
+    const uint16_t* Db, const uint16_t* Xb,
+    typename WMfma<MF>::acc_t (&acc)[BCO / WM / MF][BKK / WN / MF]) {
   constexpr int TCO = BCO / WM, TKK = BKK / WN;
-  constexpr int FM = TCO / 16, FN = TKK / 16;
   constexpr int SD = BCO, SX = BKK;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   typedef short i16x8 __attribute__((ext_vector_type(8)));
+  if constexpr (MF == 32) {
+    // lane l holds A[row l & 31][k 8 (l >> 5) + j]: 16-lane group g reads the 4 x 16 block at
+    // k rows 8 (g >> 1) + 0..3 (lo) / + 4..7 (hi), columns 16 (g & 1) + 0..15 of the fragment
+    constexpr int FM = TCO / 32, FN = TKK / 32;
+#pragma unroll
+    for (int ks = 0; ks < 2 * KS; ++ks) {
+      const int r1 = ks * 16 + 8 * (g >> 1) + q;
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int col = wm * TCO + fm * 32 + 16 * (g & 1) + 4 * pp;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Db + r1 * SD + (wg_swz<BCO, 32>(r1, col))));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Db + (r1 + 4) * SD + (wg_swz<BCO, 32>(r1 + 4, col))));
+        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[fm] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int col = wn * TKK + fn * 32 + 16 * (g & 1) + 4 * pp;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Xb + r1 * SX + (wg_swz<BKK, 32>(r1, col))));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(i16x4, Xb + (r1 + 4) * SX + (wg_swz<BKK, 32>(r1 + 4, col))));
+        i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[fn] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+    }
+    return;
+  } else {
+  constexpr int FM = TCO / 16, FN = TKK / 16;
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int r1 = ks * 32 + 8 * g + q;
@@ -1196,6 +1255,7 @@ __device__ __forceinline__ void wgrad_mma(const uint16_t* Db, const uint16_t* Xb
       for (int fn = 0; fn < FN; ++fn)
         acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
   }
+  }
 }
 
 // Sum of `cnt` float4 slabs `step` float4s apart (fixed order: four interleaved partial sums
@@ -1221,28 +1281,68 @@ __device__ __forceinline__ float4 slab_sum4(const float4* __restrict__ p, size_t
 }
 
 
-// fp32 partial slab of one split: partial[split][co][k]
-template <int BCO, int BKK, int WM, int WN>
-__device__ __forceinline__ void wgrad_store(const WgradArgs& p,
-                                            f32x4 (&acc)[BCO / WM / 16][BKK / WN / 16],
-                                            int split, int co0, int k0) {
-  constexpr int TCO = BCO / WM, TKK = BKK / WN;
-  constexpr int FM = TCO / 16, FN = TKK / 16;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid / WN, wn = wid % WN;
+// fp32 partial slab of one split: partial[split][co][k], one wave's TCO x TKK tile at
+// (cw, kw) (absolute output channel / K column of its first element)
+template <int TCO, int TKK, int MF>
+__device__ __forceinline__ void wgrad_store_at(
+    const WgradArgs& p, typename WMfma<MF>::acc_t (&acc)[TCO / MF][TKK / MF], int split, int cw,
+    int kw) {
+  constexpr int FM = TCO / MF, FN = TKK / MF;
+  const int lane = threadIdx.x & 63;
   const int g = lane >> 4, li = lane & 15;
   float* out = p.partial + (size_t)split * p.N * p.K;
+  // a whole wave tile (the usual case) stores without per-element guards: the guarded loop
+  // becomes one exec-mask branch per store (FM x FN x 16 of them per thread at 32x32)
+  const bool full = cw + TCO <= p.N && kw + TKK <= p.K;
+  if constexpr (MF == 32) {
+    // D[row][col]: col = lane & 31, row = (i & 3) + 8 (i >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int kcol = kw + fn * 32 + (lane & 31);
+        const int cob = cw + fm * 32 + 4 * (lane >> 5);
+        if (full) {
+          float* o = out + (size_t)cob * p.K + kcol;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[(size_t)((i & 3) + 8 * (i >> 2)) * p.K] = acc[fm][fn][i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int co = cob + (i & 3) + 8 * (i >> 2);
+            if (co < p.N && kcol < p.K) out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
+          }
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      const int kcol = k0 + wn * TKK + fn * 16 + li;
+      const int kcol = kw + fn * 16 + li;
+      const int cob = cw + fm * 16 + g * 4;
+      if (full) {
+        float* o = out + (size_t)cob * p.K + kcol;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int co = co0 + wm * TCO + fm * 16 + g * 4 + i;
-        if (co < p.N && kcol < p.K) out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
+        for (int i = 0; i < 4; ++i) o[(size_t)i * p.K] = acc[fm][fn][i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = cob + i;
+          if (co < p.N && kcol < p.K) out[(size_t)co * p.K + kcol] = acc[fm][fn][i];
+        }
       }
     }
+}
+
+template <int BCO, int BKK, int WM, int WN, int MF = 16>
+__device__ __forceinline__ void wgrad_store(
+    const WgradArgs& p, typename WMfma<MF>::acc_t (&acc)[BCO / WM / MF][BKK / WN / MF],
+    int split, int co0, int k0) {
+  const int wid = threadIdx.x >> 6;
+  wgrad_store_at<BCO / WM, BKK / WN, MF>(p, acc, split, co0 + (wid / WN) * (BCO / WM),
+                                         k0 + (wid % WN) * (BKK / WN));
 }
 
 // DEEP: operand loads run two 64-row steps ahead in two register sets (loop unrolled by two, every
@@ -1425,15 +1525,21 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
     if (nit > 1) gload(1, S1);
     if (nit > 2) gload(2, S0);
     __syncthreads();
+    // raw barriers: __syncthreads() emits vmcnt(0), which would drain the loads of the step
+    // two ahead (still in flight in the other register set) and reduce the pipeline to one
+    // step; the LDS hazards need only the LDS counter (the compiler waits for each register
+    // set's loads before the lstore that consumes it)
     for (int it = 0; it < nit; it += 2) {
       wgrad_mma<BCO, BKK, WM, WN>(Ds, Xs, acc);
       if (it + 1 < nit) lstore(1, S1);
-      __syncthreads();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
       if (it + 3 < nit) gload(it + 3, S1);
       if (it + 1 >= nit) break;
       wgrad_mma<BCO, BKK, WM, WN>(Ds + 64 * SD, Xs + 64 * SX, acc);
       if (it + 2 < nit) lstore(0, S0);
-      __syncthreads();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
       if (it + 4 < nit) gload(it + 4, S0);
     }
   }
@@ -1450,7 +1556,12 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 // NST LDS stages: with NST == 3 the DMA of step it+2 is issued while step it computes and a
 // counted vmcnt keeps step it+1's DMA in flight across the barrier (raw s_barrier: hipcc's
 // __syncthreads() would drain it with vmcnt(0)) — for the HBM-bound 1x1 weight gradients.
-template <int BCO, int BKK, int WM, int WN, bool PRO, int NST>
+// WG_CUT (analysis builds only, tools/wgrad_cut.sh; 0 in the shipped build): 1 = no operand DMA
+// inside the loop (MFMAs on stale tiles), 2 = no MFMAs (the DMA + barrier pipeline alone)
+#ifndef WG_CUT
+#define WG_CUT 0
+#endif
+template <int BCO, int BKK, int WM, int WN, bool PRO, int NST, int MF = 16>
 __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
   static_assert(NST == 2 || NST == 3, "wgrad_glds stages");
   constexpr int NW = WM * WN;
@@ -1486,7 +1597,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
 #pragma unroll
   for (int j = 0; j < DI; ++j) {
     const int r = (j * NW + wid) * RPD + lane / CPD;
-    const int col = co0 + tr_swz<BCO>(r, (lane % CPD) * 8);
+    const int col = co0 + wg_swz<BCO, MF>(r, (lane % CPD) * 8);
     d_row[j] = r;
     d_cok[j] = col < p.N;
     d_off[j] = (uint32_t)(((size_t)(mbeg + r) * p.N + col) * 2);
@@ -1498,7 +1609,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
 #pragma unroll
   for (int j = 0; j < XI; ++j) {
     const int r = (j * NW + wid) * RPX + lane / CPX;
-    const int kk = k0 + tr_swz<BKK>(r, (lane % CPX) * 8);
+    const int kk = k0 + wg_swz<BKK, MF>(r, (lane % CPX) * 8);
     x_row[j] = r;
     x_kok[j] = kk < p.K;
     const int tap = x_kok[j] ? kk / p.C : 0;
@@ -1544,11 +1655,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
     }
   };
 
-  f32x4 acc[BCO / WM / 16][BKK / WN / 16];
+  typename WMfma<MF>::acc_t acc[BCO / WM / MF][BKK / WN / MF];
 #pragma unroll
-  for (int i = 0; i < BCO / WM / 16; ++i)
+  for (int i = 0; i < BCO / WM / MF; ++i)
 #pragma unroll
-    for (int j = 0; j < BKK / WN / 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < BKK / WN / MF; ++j) acc[i][j] = {};
 
   constexpr int PER = DI + XI;  // DMA instructions per wave per step
   if (PRO) {
@@ -1565,11 +1676,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
   constexpr int PXC = 64 * CPX / (64 * NW);  // X-prologue chunks per thread per step
   // the thread's chunks share their tr_swz key (row bits 0-3) when they are 16k rows apart;
   // the 32 table registers only where the accumulators leave room (256 x 256: 128 of them)
-  constexpr bool HOIST = (64 * NW / CPX) % 16 == 0 && (BCO / WM / 16) * (BKK / WN / 16) * 4 <= 64;
+  constexpr bool HOIST = (64 * NW / CPX) % 16 == 0 && (BCO / WM) * (BKK / WN) / 64 <= 64;
   const int ptc = tid % CPX;                             // the thread's physical chunk
   float pro_sc0[8], pro_sh0[8], pro_sc1[8], pro_sh1[8];  // its logical column's tables
   if (PRO && HOIST) {
-    const int col = tr_swz<BKK>(tid / CPX, ptc * 8);
+    const int col = wg_swz<BKK, MF>(tid / CPX, ptc * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       pro_sc0[e] = Pt[col + e];
@@ -1588,7 +1699,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // step it landed for every wave; buffer (it-1) % NST is free
-    if (NST > 1 && it + NST - 1 < nit) issue(it + NST - 1, (it + NST - 1) % NST);
+    if (WG_CUT != 1 && NST > 1 && it + NST - 1 < nit) issue(it + NST - 1, (it + NST - 1) % NST);
     if (PRO && !HOIST) {
       // rows past mend hold zero dY, so whatever the transform makes of them contributes 0;
       // columns past K are dropped by the store
@@ -1597,7 +1708,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
       for (int i = 0; i < PXC; ++i) {
         const int c = tid + i * 64 * NW;
         const int row = c / CPX, pc = c % CPX;
-        const int col = tr_swz<BKK>(row, pc * 8);
+        const int col = wg_swz<BKK, MF>(row, pc * 8);
         const int sg = (p.pro_S > 1 && mb + row >= p.pro_seg_rows) ? 1 : 0;
         const float4* ps = (const float4*)(Pt + sg * BKK + col);
         const float4* ph = (const float4*)(Pt + (2 + sg) * BKK + col);
@@ -1641,9 +1752,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
-    wgrad_mma<BCO, BKK, WM, WN>(Ds + cur * 64 * BCO, Xs + cur * 64 * BKK, acc);
+    if (WG_CUT != 2) wgrad_mma<BCO, BKK, WM, WN, 2, MF>(Ds + cur * 64 * BCO, Xs + cur * 64 * BKK, acc);
   }
-  wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
+  wgrad_store<BCO, BKK, WM, WN, MF>(p, acc, split, co0, k0);
 }
 
 // Deep-pipelined LDS-DMA weight gradient (no operand prologues).  wgrad_glds stages 64-row
@@ -1657,7 +1768,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
 // across barriers"); the barrier also publishes that every wave's fragment reads of the buffer
 // being refilled have retired (lgkmcnt(0) before it).  s_setprio(1) around the MFMA cluster
 // keeps hipcc from hoisting MFMAs across the barriers.
-template <int BCO, int BKK, int WM, int WN, int SR, int NST>
+template <int BCO, int BKK, int WM, int WN, int SR, int NST, int MF = 16>
 __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_pipe(WgradArgs p) {
   constexpr int NW = WM * WN;
   constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = SR / (RPD * NW);
@@ -1693,7 +1804,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_pipe(WgradArgs p) {
 #pragma unroll
   for (int j = 0; j < DI; ++j) {
     const int r = (j * NW + wid) * RPD + lane / CPD;
-    const int col = co0 + tr_swz<BCO>(r, (lane % CPD) * 8);
+    const int col = co0 + wg_swz<BCO, MF>(r, (lane % CPD) * 8);
     d_row[j] = r;
     d_cok[j] = col < p.N;
     d_off[j] = (uint32_t)(((size_t)(mbeg + r) * p.N + col) * 2);
@@ -1704,7 +1815,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_pipe(WgradArgs p) {
 #pragma unroll
   for (int j = 0; j < XI; ++j) {
     const int r = (j * NW + wid) * RPX + lane / CPX;
-    const int kk = k0 + tr_swz<BKK>(r, (lane % CPX) * 8);
+    const int kk = k0 + wg_swz<BKK, MF>(r, (lane % CPX) * 8);
     x_row[j] = r;
     x_kok[j] = kk < p.K;
     const int tap = x_kok[j] ? kk / p.C : 0;
@@ -1750,11 +1861,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_pipe(WgradArgs p) {
     }
   };
 
-  f32x4 acc[BCO / WM / 16][BKK / WN / 16];
+  typename WMfma<MF>::acc_t acc[BCO / WM / MF][BKK / WN / MF];
 #pragma unroll
-  for (int i = 0; i < BCO / WM / 16; ++i)
+  for (int i = 0; i < BCO / WM / MF; ++i)
 #pragma unroll
-    for (int j = 0; j < BKK / WN / 16; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < BKK / WN / MF; ++j) acc[i][j] = {};
 
 #pragma unroll
   for (int j = 0; j < NST - 1; ++j)
@@ -1778,11 +1889,246 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_pipe(WgradArgs p) {
       issue(it + NST - 1, nb);
     }
     __builtin_amdgcn_s_setprio(1);
-    wgrad_mma<BCO, BKK, WM, WN, SR / 32>(Ds + cur * SR * BCO, Xs + cur * SR * BKK, acc);
+    wgrad_mma<BCO, BKK, WM, WN, SR / 32, MF>(Ds + cur * SR * BCO, Xs + cur * SR * BKK, acc);
     __builtin_amdgcn_s_setprio(0);
     cur = cur + 1 == NST ? 0 : cur + 1;
   }
-  wgrad_store<BCO, BKK, WM, WN>(p, acc, split, co0, k0);
+  wgrad_store<BCO, BKK, WM, WN, MF>(p, acc, split, co0, k0);
+}
+
+// Ping-pong weight gradient.  In wgrad_glds / wgrad_pipe every wave reads
+// its fragments and then runs its MFMAs between the same two barriers, so right after each
+// barrier all waves of a CU wait on LDS reads together and the MFMA pipes idle (the compute half
+// alone, no global traffic, ran at ~55 % of the MFMA rate: r4 optimisation log, cut-down builds).
+// Here the 8 waves form two groups of 4, one wave of each per SIMD, that trade roles every
+// phase (one raw barrier per phase):
+//   phase A of step s: group 0 issues the DMA of step s + NST - 1 and reads step s's fragments;
+//                      group 1 runs the MFMAs of step s - 1 (fragments read in its phase B)
+//   phase B of step s: group 0 runs step s's MFMAs; group 1 reads step s's fragments
+// so every SIMD always has one wave in an MFMA phase beside one in a read phase.  A step is
+// SR = 32 rows; group 0 (the loaders) keeps NST - 1 steps of DMA in flight (counted vmcnt before
+// the barrier that opens the phase A needing the data, never vmcnt(0) in the loop).  Buffer
+// reuse: the DMA into step s - 1's buffer is issued in phase A of step s, after group 1's reads
+// of it retired (lgkmcnt(0) before the phase B barrier).  sched_barrier pins each phase's
+// instructions between its barriers.  Group g owns output channels [g BCO / 2, (g + 1) BCO / 2)
+// as 2 x 2 waves of (BCO / 4) x (BKK / 2).  No operand prologues.
+template <int TCO, int TKK, int SD, int SX, int MF>
+struct WgFrags {
+  static constexpr int NKS = MF == 16 ? 1 : 2;  // k sub-steps of one 32-row step
+  bf16x8 a[NKS][TCO / MF], b[NKS][TKK / MF];
+};
+
+template <int TCO, int TKK, int SD, int SX, int MF>
+__device__ __forceinline__ void wg_read32(const uint16_t* Db, const uint16_t* Xb, int co_w, int kk_w,
+                                          WgFrags<TCO, TKK, SD, SX, MF>& f) {
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+#pragma unroll
+  for (int ks = 0; ks < WgFrags<TCO, TKK, SD, SX, MF>::NKS; ++ks) {
+    // MF 16: rows 8g + q (+4), columns 16 fm + 4pp; MF 32: rows 16 ks + 8 (g >> 1) + q (+4),
+    // columns 32 fm + 16 (g & 1) + 4pp (see wgrad_mma)
+    const int r1 = MF == 16 ? 8 * g + q : ks * 16 + 8 * (g >> 1) + q;
+    const int cg = MF == 16 ? 4 * pp : 16 * (g & 1) + 4 * pp;
+#pragma unroll
+    for (int fm = 0; fm < TCO / MF; ++fm) {
+      const int col = co_w + fm * MF + cg;
+      i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Db + r1 * SD + (wg_swz<SD, MF>(r1, col))));
+      i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Db + (r1 + 4) * SD + (wg_swz<SD, MF>(r1 + 4, col))));
+      i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      f.a[ks][fm] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int fn = 0; fn < TKK / MF; ++fn) {
+      const int col = kk_w + fn * MF + cg;
+      i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Xb + r1 * SX + (wg_swz<SX, MF>(r1, col))));
+      i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          LDS_PTR(i16x4, Xb + (r1 + 4) * SX + (wg_swz<SX, MF>(r1 + 4, col))));
+      i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      f.b[ks][fn] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+}
+
+template <int TCO, int TKK, int SD, int SX, int MF>
+__device__ __forceinline__ void wg_mfma32(const WgFrags<TCO, TKK, SD, SX, MF>& f,
+                                          typename WMfma<MF>::acc_t (&acc)[TCO / MF][TKK / MF]) {
+#pragma unroll
+  for (int ks = 0; ks < WgFrags<TCO, TKK, SD, SX, MF>::NKS; ++ks)
+#pragma unroll
+    for (int fm = 0; fm < TCO / MF; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < TKK / MF; ++fn) {
+        if constexpr (MF == 16)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[ks][fm], f.b[ks][fn],
+                                                                acc[fm][fn], 0, 0, 0);
+        else
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[ks][fm], f.b[ks][fn],
+                                                                acc[fm][fn], 0, 0, 0);
+      }
+}
+
+#define WG_PHASE_BARRIER()                               \
+  do {                                                   \
+    __builtin_amdgcn_sched_barrier(0);                   \
+    __builtin_amdgcn_s_barrier();                        \
+    __builtin_amdgcn_sched_barrier(0);                   \
+  } while (0)
+
+template <int BCO, int BKK, int MF, int NST>
+__global__ __launch_bounds__(512, 1) void wgrad_pp(WgradArgs p) {
+  constexpr int SR = 32, NL = 4;  // rows per step, loader waves (group 0)
+  constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = SR / (RPD * NL);
+  constexpr int CPX = BKK / 8, RPX = 64 / CPX, XI = SR / (RPX * NL);
+  static_assert(DI >= 1 && XI >= 1 && DI * RPD * NL == SR && XI * RPX * NL == SR, "pp mapping");
+  static_assert(NST >= 3 && NST <= 5, "wgrad_pp stages");
+  constexpr int PER = DI + XI;  // DMA instructions per loader wave per step
+  constexpr int TCO = BCO / 4, TKK = BKK / 2;
+  static_assert(TCO % MF == 0 && TKK % MF == 0, "wave tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ds = (uint16_t*)smem;      // [NST][SR][BCO]
+  uint16_t* Xs = Ds + NST * SR * BCO;  // [NST][SR][BKK]
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int grp = wid >> 2, w4 = wid & 3;
+  const int co_w = grp * (BCO / 2) + (w4 >> 1) * TCO;
+  const int kk_w = (w4 & 1) * TKK;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = p.nCo * p.nKk;
+  const int split = lbid / tiles;
+  const int tile = lbid % tiles;
+  const int co0 = (tile / p.nKk) * BCO;
+  const int k0 = (tile % p.nKk) * BKK;
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, (int)p.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
+  const int mbeg = split * p.iters_per_split * 64;  // host splits in 64-row units
+  const int mend_raw = mbeg + p.iters_per_split * 64;
+  const int mend = mend_raw < p.M ? mend_raw : p.M;
+  const int nit = mend > mbeg ? (mend - mbeg + SR - 1) / SR : 0;
+  const int OHW = p.OH * p.OW;
+
+  // loader addressing (meaningful in group 0; computed by every wave, uniform control flow)
+  int d_row[DI];
+  uint32_t d_off[DI];
+  bool d_cok[DI];
+#pragma unroll
+  for (int j = 0; j < DI; ++j) {
+    const int r = (j * NL + w4) * RPD + lane / CPD;
+    const int col = co0 + wg_swz<BCO, MF>(r, (lane % CPD) * 8);
+    d_row[j] = r;
+    d_cok[j] = col < p.N;
+    d_off[j] = (uint32_t)(((size_t)(mbeg + r) * p.N + col) * 2);
+  }
+  const uint32_t dstep = (uint32_t)(SR * p.N * 2);
+  int x_row[XI], x_ci[XI], x_ihb[XI], x_iwb[XI], xn[XI], xoh[XI], xow[XI];
+  bool x_kok[XI];
+#pragma unroll
+  for (int j = 0; j < XI; ++j) {
+    const int r = (j * NL + w4) * RPX + lane / CPX;
+    const int kk = k0 + wg_swz<BKK, MF>(r, (lane % CPX) * 8);
+    x_row[j] = r;
+    x_kok[j] = kk < p.K;
+    const int tap = x_kok[j] ? kk / p.C : 0;
+    x_ci[j] = kk - tap * p.C;
+    const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+    x_ihb[j] = p.ih0 + kh * p.dh;
+    x_iwb[j] = p.iw0 + kw * p.dw;
+    const int m = mbeg + r;
+    xn[j] = m / OHW;
+    const int rem = m - xn[j] * OHW;
+    xoh[j] = rem / p.OW;
+    xow[j] = rem - xoh[j] * p.OW;
+  }
+  const int dn = SR / OHW, dr = SR - dn * OHW;
+  const int doh = dr / p.OW, dow = dr - doh * p.OW;
+  const int cstride = p.C * 2;
+
+  auto issue = [&](int it, int buf) {
+    const int mb = mbeg + it * SR;
+#pragma unroll
+    for (int j = 0; j < DI; ++j) {
+      const bool ok = mb + d_row[j] < mend && d_cok[j];
+      dma16_opaque(rd, Ds + buf * SR * BCO + (j * NL + w4) * RPD * BCO, ok ? d_off[j] : p.dy_bytes);
+      d_off[j] += dstep;
+    }
+#pragma unroll
+    for (int j = 0; j < XI; ++j) {
+      const int ih = (int)__umul24((unsigned)xoh[j], (unsigned)p.ish) + x_ihb[j];
+      const int iw = (int)__umul24((unsigned)xow[j], (unsigned)p.isw) + x_iwb[j];
+      const bool ok = mb + x_row[j] < mend && x_kok[j] && (unsigned)ih < (unsigned)p.IH &&
+                      (unsigned)iw < (unsigned)p.IW;
+      const uint32_t pix =
+          __umul24(__umul24((unsigned)xn[j], (unsigned)p.IH) + (unsigned)ih, (unsigned)p.IW) +
+          (unsigned)iw;
+      const uint32_t off = ok ? __umul24(pix, (unsigned)cstride) + (uint32_t)(x_ci[j] * 2)
+                              : p.x_bytes;
+      dma16_opaque(rx, Xs + buf * SR * BKK + (j * NL + w4) * RPX * BKK, off);
+      int ow = xow[j] + dow, oh = xoh[j] + doh, n = xn[j] + dn;
+      if (ow >= p.OW) { ow -= p.OW; ++oh; }
+      if (oh >= p.OH) { oh -= p.OH; ++n; }
+      xow[j] = ow; xoh[j] = oh; xn[j] = n;
+    }
+  };
+  // group 0: wait until step `next` landed, with the steps after it (up to NST - 2) in flight
+  auto wait_step = [&](int next) {
+    const int ahead = min(NST - 2, nit - 1 - next);
+    if (ahead >= NST - 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (NST - 2)) : "memory");
+    else if (NST > 3 && ahead == 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * 2) : "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  typename WMfma<MF>::acc_t acc[TCO / MF][TKK / MF];
+#pragma unroll
+  for (int i = 0; i < TCO / MF; ++i)
+#pragma unroll
+    for (int j = 0; j < TKK / MF; ++j) acc[i][j] = {};
+  WgFrags<TCO, TKK, BCO, BKK, MF> fr;
+
+  if (grp == 0) {
+#pragma unroll
+    for (int j = 0; j < NST - 1; ++j)
+      if (j < nit) issue(j, j);
+    if (nit > 0) wait_step(0);
+  }
+  WG_PHASE_BARRIER();
+  int cur = 0;
+  for (int s = 0; s < nit; ++s) {
+    // phase A
+    if (grp == 0) {
+      if (s + NST - 1 < nit) issue(s + NST - 1, cur == 0 ? NST - 1 : cur - 1);
+      wg_read32<TCO, TKK, BCO, BKK, MF>(Ds + cur * SR * BCO, Xs + cur * SR * BKK, co_w, kk_w, fr);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else if (s > 0) {
+      __builtin_amdgcn_s_setprio(1);
+      wg_mfma32<TCO, TKK, BCO, BKK, MF>(fr, acc);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    WG_PHASE_BARRIER();
+    // phase B
+    if (grp == 0) {
+      __builtin_amdgcn_s_setprio(1);
+      wg_mfma32<TCO, TKK, BCO, BKK, MF>(fr, acc);
+      __builtin_amdgcn_s_setprio(0);
+      if (s + 1 < nit) wait_step(s + 1);
+    } else {
+      wg_read32<TCO, TKK, BCO, BKK, MF>(Ds + cur * SR * BCO, Xs + cur * SR * BKK, co_w, kk_w, fr);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    WG_PHASE_BARRIER();
+    cur = cur + 1 == NST ? 0 : cur + 1;
+  }
+  if (grp == 1 && nit > 0) wg_mfma32<TCO, TKK, BCO, BKK, MF>(fr, acc);
+  wgrad_store_at<TCO, TKK, MF>(p, acc, split, co0 + co_w, k0 + kk_w);
 }
 
 // Weight gradient of a 3x3 / stride-1 / pad-1 convolution (16x16 / 32x32, C in {64, 128}) with
@@ -2295,30 +2641,45 @@ void launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
-template <int BCO, int BKK, int WM, int WN, int SR, int NST>
+template <int BCO, int BKK, int WM, int WN, int SR, int NST, int MF = 16>
 void launch_wgrad_pipe(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   a.nCo = (a.N + BCO - 1) / BCO;
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
   const size_t lds = (size_t)NST * SR * (BCO + BKK) * 2;
-  hipLaunchKernelGGL((wgrad_pipe<BCO, BKK, WM, WN, SR, NST>), dim3(grid), dim3(64 * WM * WN),
+  hipLaunchKernelGGL((wgrad_pipe<BCO, BKK, WM, WN, SR, NST, MF>), dim3(grid), dim3(64 * WM * WN),
                      lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
-template <int BCO, int BKK, int WM, int WN, int NST = 2>
+// PRO_OK false: the X-operand prologue is not instantiated (it spills; wgrad_variant_ok rejects it)
+template <int BCO, int BKK, int MF, int NST>
+void launch_wgrad_pp(const WgradArgs& a0, hipStream_t s) {
+  WgradArgs a = a0;
+  a.nCo = (a.N + BCO - 1) / BCO;
+  a.nKk = (a.K + BKK - 1) / BKK;
+  const int grid = a.nCo * a.nKk * a.splits;
+  const size_t lds = (size_t)NST * 32 * (BCO + BKK) * 2;
+  hipLaunchKernelGGL((wgrad_pp<BCO, BKK, MF, NST>), dim3(grid), dim3(512), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
+template <int BCO, int BKK, int WM, int WN, int NST = 2, int MF = 16, bool PRO_OK = true>
 void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   a.nCo = (a.N + BCO - 1) / BCO;
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
   const size_t lds = (size_t)NST * 64 * (BCO + BKK) * 2 + (a.pro_sc != nullptr ? 16 * BKK : 0);
-  if (a.pro_sc != nullptr)
-    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, true, NST>), dim3(grid), dim3(64 * WM * WN),
+  if constexpr (!PRO_OK)
+    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, false, NST, MF>), dim3(grid),
+                       dim3(64 * WM * WN), lds, s, a);
+  else if (a.pro_sc != nullptr)
+    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, true, NST, MF>), dim3(grid), dim3(64 * WM * WN),
                        lds, s, a);
   else
-    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, false, NST>), dim3(grid), dim3(64 * WM * WN),
+    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, false, NST, MF>), dim3(grid), dim3(64 * WM * WN),
                        lds, s, a);
   HIP_CHECK_LAUNCH();
 }
@@ -2354,7 +2715,11 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {128, 64, 512},  {128, 128, 256}, {64, 128, 512},
                                   {256, 128, 256}, {64, 64, 256},
                                   {64, 128, 768}, {128, 64, 768},
-                                  {256, 256, 256}, {256, 128, 256}, {128, 256, 256}};
+                                  {256, 256, 256}, {256, 128, 256}, {128, 256, 256},
+                                  {256, 256, 256}, {256, 128, 256}, {128, 256, 256},
+                                  {256, 256, 256}, {256, 256, 256}, {256, 256, 256},
+                                  {128, 128, 512}, {128, 256, 256}, {256, 128, 256},
+                                  {256, 256, 256}, {128, 256, 256}, {256, 128, 256}};
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 // wgrad_tn with loads two steps ahead (DEEP): the 64 x 128 / 128 x 64 tiles gain 10-17 % on the
@@ -2363,6 +2728,18 @@ constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one i
 constexpr int WG_DEEP0 = 18;
 // 20-22: wgrad_pipe (32-row steps, 4-5 LDS stages with all but one in flight), no prologues
 constexpr int WG_PIPE0 = 20;
+// 23-27: wgrad_glds on v_mfma_f32_32x32x16_bf16 (23-25: the 8-wave / 4-wave tiles of 9, 7, 8;
+// 27: 4 waves of 128 x 128) and 26: 4 waves of 128 x 128 on 16x16x32 — the 128 x 128 wave tile
+// reads 2/3 of the LDS fragment bytes per FLOP of a 128 x 64 one; X-operand prologue allowed
+// (not on 26: it spills there)
+constexpr int WG_GLDS32 = 23;
+// 28, 30, 31: wgrad_pipe 256 x 256 / 128 x 256 / 256 x 128 (8 waves) on 32x32x16 (as 20, 22, 21)
+constexpr int WG_PIPE32 = 28;
+// 29: wgrad_glds 128 x 128 (4 waves) on 32x32x16 (as 6), X-operand prologue allowed
+constexpr int WG_GLDS32B = 29;
+// 32-34: wgrad_pp (two wave groups trading read / MFMA phases), 16x16x32, tiles 256 x 256,
+// 128 x 256, 256 x 128 (the 32x32x16 form spills there); no prologues
+constexpr int WG_PP0 = 32;
 
 
 // -------------------------------------------------- fused 1x1 backward: dgrad + wgrad in one pass
@@ -2547,19 +2924,24 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
   }
   if (T > 1) gload(1, rG[1], rA[1], rX[1]);
   __syncthreads();
+  // raw barriers (LDS counter only): __syncthreads() emits vmcnt(0), which would drain the
+  // loads of tile t + 2 issued at the top of the iteration and leave one tile in flight
   for (int t = 0; t < T; t += 2) {
     // even tile t: set 1 holds t + 1, set 0 is free
     if (t + 2 < T) gload(t + 2, rG[0], rA[0], rX[0]);
     compute(t);
     if (t + 1 < T) lstore(1, rG[1], rA[1], rX[1]);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (t + 1 >= T) break;
     // odd tile t + 1: set 0 holds t + 2, set 1 is free
     if (t + 3 < T) gload(t + 3, rG[1], rA[1], rX[1]);
     compute(t + 1);
     if (t + 2 < T) lstore(0, rG[0], rA[0], rX[0]);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
+  __syncthreads();
   // dW slab of this block: [co][ci]
   float* wp = p.wpart + (size_t)blk * CO * CI;
 #pragma unroll
@@ -2726,6 +3108,8 @@ bool wgrad_variant_glds(int v) { return (v >= WG_GLDS0 && v < WG_PATCH0) || v >=
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
   if (v == WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
+  if ((v >= WG_GLDS32 && v < WG_PIPE32) || v == WG_GLDS32B)
+    return !dy_pro && !(pro && v == WG_GLDS32 + 3) && igemm_glds_ok(g, pro, false);
   if (v >= WG_PIPE0) return !dy_pro && !pro && igemm_glds_ok(g, false, false);
   if (v >= WG_DEEP0) return true;  // register-staged: every prologue
   // wgrad_glds has the X-operand BN-apply prologue only (no dY BN-backward prologue)
@@ -2833,6 +3217,18 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 20: launch_wgrad_pipe<256, 256, 2, 4, 32, 4>(a, s); break;
     case 21: launch_wgrad_pipe<256, 128, 4, 2, 32, 5>(a, s); break;
     case 22: launch_wgrad_pipe<128, 256, 2, 4, 32, 5>(a, s); break;
+    case 23: launch_wgrad_glds<256, 256, 2, 4, 2, 32>(a, s); break;
+    case 24: launch_wgrad_glds<256, 128, 2, 2, 2, 32>(a, s); break;
+    case 25: launch_wgrad_glds<128, 256, 2, 2, 2, 32>(a, s); break;
+    case 26: launch_wgrad_glds<256, 256, 2, 2, 2, 16, false>(a, s); break;
+    case 27: launch_wgrad_glds<256, 256, 2, 2, 2, 32>(a, s); break;
+    case 28: launch_wgrad_pipe<256, 256, 2, 4, 32, 4, 32>(a, s); break;
+    case 29: launch_wgrad_glds<128, 128, 2, 2, 2, 32>(a, s); break;
+    case 30: launch_wgrad_pipe<128, 256, 2, 4, 32, 5, 32>(a, s); break;
+    case 31: launch_wgrad_pipe<256, 128, 4, 2, 32, 5, 32>(a, s); break;
+    case 32: launch_wgrad_pp<256, 256, 16, 4>(a, s); break;
+    case 33: launch_wgrad_pp<128, 256, 16, 4>(a, s); break;
+    case 34: launch_wgrad_pp<256, 128, 16, 4>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;

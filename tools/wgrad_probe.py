@@ -1,5 +1,7 @@
 """Run ONE weight-gradient launch configuration repeatedly (for rocprofv3 --pmc / kernel-trace
-per-variant analysis).  Usage: python tools/wgrad_probe.py N C H Co k s p [variant|-1] [reps]"""
+per-variant analysis).  Usage: python tools/wgrad_probe.py N C H Co k s p [variant|-1|v1,v2,..]
+[reps] [rounds] — a list is timed in `rounds` interleaved rounds (box clock drift hits every arm);
+variants the geometry does not admit are skipped."""
 import sys
 from pathlib import Path
 
@@ -8,7 +10,7 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
-def main(N, C, H, Co, k, s, p, variant=-1, reps=20):
+def main(N, C, H, Co, k, s, p, variant=-1, reps=20, rounds=1):
     from simclr_amd.ops import _ext
     from simclr_amd.ops.conv_hip import fwd_geom
     ops = _ext.ops()
@@ -17,11 +19,12 @@ def main(N, C, H, Co, k, s, p, variant=-1, reps=20):
     x = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
     dy = torch.randn(N, OH, OH, Co, device=dev).to(torch.bfloat16)
     g = fwd_geom(N, H, H, C, OH, OH, k, k, s, p, Co)
-    vs = [variant] if variant >= 0 else [v for v in range(ops.wgrad_nvariants())
-                                         if ops.wgrad_variant_ok(v, g, False, False)]
+    vs = (list(variant) if isinstance(variant, (list, tuple)) else
+          [variant] if variant >= 0 else list(range(ops.wgrad_nvariants())))
+    vs = [v for v in vs if ops.wgrad_variant_ok(v, g, False, False)]
     out = torch.empty(Co, k, k, C, device=dev)
     flop = 2.0 * N * OH * OH * Co * k * k * C
-    for v in vs:
+    for v in [v for _ in range(rounds) for v in vs]:
         sp = ops.wgrad_splits(g, v)
         part = torch.empty(sp * Co * k * k * C, device=dev)
         ops.wgrad(dy, x, part, out, g, sp, C, 0.0, None, None, 0, False, 1, v)
@@ -39,5 +42,5 @@ def main(N, C, H, Co, k, s, p, variant=-1, reps=20):
 
 
 if __name__ == "__main__":
-    a = [int(v) for v in sys.argv[1:]]
+    a = [[int(x) for x in v.split(",")] if "," in v else int(v) for v in sys.argv[1:]]
     main(*a)
