@@ -1896,241 +1896,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_pipe(WgradArgs p) {
   wgrad_store<BCO, BKK, WM, WN, MF>(p, acc, split, co0, k0);
 }
 
-// Ping-pong weight gradient.  In wgrad_glds / wgrad_pipe every wave reads
-// its fragments and then runs its MFMAs between the same two barriers, so right after each
-// barrier all waves of a CU wait on LDS reads together and the MFMA pipes idle (the compute half
-// alone, no global traffic, ran at ~55 % of the MFMA rate: r4 optimisation log, cut-down builds).
-// Here the 8 waves form two groups of 4, one wave of each per SIMD, that trade roles every
-// phase (one raw barrier per phase):
-//   phase A of step s: group 0 issues the DMA of step s + NST - 1 and reads step s's fragments;
-//                      group 1 runs the MFMAs of step s - 1 (fragments read in its phase B)
-//   phase B of step s: group 0 runs step s's MFMAs; group 1 reads step s's fragments
-// so every SIMD always has one wave in an MFMA phase beside one in a read phase.  A step is
-// SR = 32 rows; group 0 (the loaders) keeps NST - 1 steps of DMA in flight (counted vmcnt before
-// the barrier that opens the phase A needing the data, never vmcnt(0) in the loop).  Buffer
-// reuse: the DMA into step s - 1's buffer is issued in phase A of step s, after group 1's reads
-// of it retired (lgkmcnt(0) before the phase B barrier).  sched_barrier pins each phase's
-// instructions between its barriers.  Group g owns output channels [g BCO / 2, (g + 1) BCO / 2)
-// as 2 x 2 waves of (BCO / 4) x (BKK / 2).  No operand prologues.
-template <int TCO, int TKK, int SD, int SX, int MF>
-struct WgFrags {
-  static constexpr int NKS = MF == 16 ? 1 : 2;  // k sub-steps of one 32-row step
-  bf16x8 a[NKS][TCO / MF], b[NKS][TKK / MF];
-};
-
-template <int TCO, int TKK, int SD, int SX, int MF>
-__device__ __forceinline__ void wg_read32(const uint16_t* Db, const uint16_t* Xb, int co_w, int kk_w,
-                                          WgFrags<TCO, TKK, SD, SX, MF>& f) {
-  typedef short i16x8 __attribute__((ext_vector_type(8)));
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-#pragma unroll
-  for (int ks = 0; ks < WgFrags<TCO, TKK, SD, SX, MF>::NKS; ++ks) {
-    // MF 16: rows 8g + q (+4), columns 16 fm + 4pp; MF 32: rows 16 ks + 8 (g >> 1) + q (+4),
-    // columns 32 fm + 16 (g & 1) + 4pp (see wgrad_mma)
-    const int r1 = MF == 16 ? 8 * g + q : ks * 16 + 8 * (g >> 1) + q;
-    const int cg = MF == 16 ? 4 * pp : 16 * (g & 1) + 4 * pp;
-#pragma unroll
-    for (int fm = 0; fm < TCO / MF; ++fm) {
-      const int col = co_w + fm * MF + cg;
-      i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          LDS_PTR(i16x4, Db + r1 * SD + (wg_swz<SD, MF>(r1, col))));
-      i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          LDS_PTR(i16x4, Db + (r1 + 4) * SD + (wg_swz<SD, MF>(r1 + 4, col))));
-      i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      f.a[ks][fm] = __builtin_bit_cast(bf16x8, v);
-    }
-#pragma unroll
-    for (int fn = 0; fn < TKK / MF; ++fn) {
-      const int col = kk_w + fn * MF + cg;
-      i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          LDS_PTR(i16x4, Xb + r1 * SX + (wg_swz<SX, MF>(r1, col))));
-      i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          LDS_PTR(i16x4, Xb + (r1 + 4) * SX + (wg_swz<SX, MF>(r1 + 4, col))));
-      i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      f.b[ks][fn] = __builtin_bit_cast(bf16x8, v);
-    }
-  }
-}
-
-template <int TCO, int TKK, int SD, int SX, int MF>
-__device__ __forceinline__ void wg_mfma32(const WgFrags<TCO, TKK, SD, SX, MF>& f,
-                                          typename WMfma<MF>::acc_t (&acc)[TCO / MF][TKK / MF]) {
-#pragma unroll
-  for (int ks = 0; ks < WgFrags<TCO, TKK, SD, SX, MF>::NKS; ++ks)
-#pragma unroll
-    for (int fm = 0; fm < TCO / MF; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < TKK / MF; ++fn) {
-        if constexpr (MF == 16)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[ks][fm], f.b[ks][fn],
-                                                                acc[fm][fn], 0, 0, 0);
-        else
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[ks][fm], f.b[ks][fn],
-                                                                acc[fm][fn], 0, 0, 0);
-      }
-}
-
-#define WG_PHASE_BARRIER()                               \
-  do {                                                   \
-    __builtin_amdgcn_sched_barrier(0);                   \
-    __builtin_amdgcn_s_barrier();                        \
-    __builtin_amdgcn_sched_barrier(0);                   \
-  } while (0)
-
-template <int BCO, int BKK, int MF, int NST>
-__global__ __launch_bounds__(512, 1) void wgrad_pp(WgradArgs p) {
-  constexpr int SR = 32, NL = 4;  // rows per step, loader waves (group 0)
-  constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = SR / (RPD * NL);
-  constexpr int CPX = BKK / 8, RPX = 64 / CPX, XI = SR / (RPX * NL);
-  static_assert(DI >= 1 && XI >= 1 && DI * RPD * NL == SR && XI * RPX * NL == SR, "pp mapping");
-  static_assert(NST >= 3 && NST <= 5, "wgrad_pp stages");
-  constexpr int PER = DI + XI;  // DMA instructions per loader wave per step
-  constexpr int TCO = BCO / 4, TKK = BKK / 2;
-  static_assert(TCO % MF == 0 && TKK % MF == 0, "wave tile");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* Ds = (uint16_t*)smem;      // [NST][SR][BCO]
-  uint16_t* Xs = Ds + NST * SR * BCO;  // [NST][SR][BKK]
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int grp = wid >> 2, w4 = wid & 3;
-  const int co_w = grp * (BCO / 2) + (w4 >> 1) * TCO;
-  const int kk_w = (w4 & 1) * TKK;
-  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tiles = p.nCo * p.nKk;
-  const int split = lbid / tiles;
-  const int tile = lbid % tiles;
-  const int co0 = (tile / p.nKk) * BCO;
-  const int k0 = (tile % p.nKk) * BKK;
-  const __amdgpu_buffer_rsrc_t rd =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, (int)p.dy_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
-  const int mbeg = split * p.iters_per_split * 64;  // host splits in 64-row units
-  const int mend_raw = mbeg + p.iters_per_split * 64;
-  const int mend = mend_raw < p.M ? mend_raw : p.M;
-  const int nit = mend > mbeg ? (mend - mbeg + SR - 1) / SR : 0;
-  const int OHW = p.OH * p.OW;
-
-  // loader addressing (meaningful in group 0; computed by every wave, uniform control flow)
-  int d_row[DI];
-  uint32_t d_off[DI];
-  bool d_cok[DI];
-#pragma unroll
-  for (int j = 0; j < DI; ++j) {
-    const int r = (j * NL + w4) * RPD + lane / CPD;
-    const int col = co0 + wg_swz<BCO, MF>(r, (lane % CPD) * 8);
-    d_row[j] = r;
-    d_cok[j] = col < p.N;
-    d_off[j] = (uint32_t)(((size_t)(mbeg + r) * p.N + col) * 2);
-  }
-  const uint32_t dstep = (uint32_t)(SR * p.N * 2);
-  int x_row[XI], x_ci[XI], x_ihb[XI], x_iwb[XI], xn[XI], xoh[XI], xow[XI];
-  bool x_kok[XI];
-#pragma unroll
-  for (int j = 0; j < XI; ++j) {
-    const int r = (j * NL + w4) * RPX + lane / CPX;
-    const int kk = k0 + wg_swz<BKK, MF>(r, (lane % CPX) * 8);
-    x_row[j] = r;
-    x_kok[j] = kk < p.K;
-    const int tap = x_kok[j] ? kk / p.C : 0;
-    x_ci[j] = kk - tap * p.C;
-    const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
-    x_ihb[j] = p.ih0 + kh * p.dh;
-    x_iwb[j] = p.iw0 + kw * p.dw;
-    const int m = mbeg + r;
-    xn[j] = m / OHW;
-    const int rem = m - xn[j] * OHW;
-    xoh[j] = rem / p.OW;
-    xow[j] = rem - xoh[j] * p.OW;
-  }
-  const int dn = SR / OHW, dr = SR - dn * OHW;
-  const int doh = dr / p.OW, dow = dr - doh * p.OW;
-  const int cstride = p.C * 2;
-
-  auto issue = [&](int it, int buf) {
-    const int mb = mbeg + it * SR;
-#pragma unroll
-    for (int j = 0; j < DI; ++j) {
-      const bool ok = mb + d_row[j] < mend && d_cok[j];
-      dma16_opaque(rd, Ds + buf * SR * BCO + (j * NL + w4) * RPD * BCO, ok ? d_off[j] : p.dy_bytes);
-      d_off[j] += dstep;
-    }
-#pragma unroll
-    for (int j = 0; j < XI; ++j) {
-      const int ih = (int)__umul24((unsigned)xoh[j], (unsigned)p.ish) + x_ihb[j];
-      const int iw = (int)__umul24((unsigned)xow[j], (unsigned)p.isw) + x_iwb[j];
-      const bool ok = mb + x_row[j] < mend && x_kok[j] && (unsigned)ih < (unsigned)p.IH &&
-                      (unsigned)iw < (unsigned)p.IW;
-      const uint32_t pix =
-          __umul24(__umul24((unsigned)xn[j], (unsigned)p.IH) + (unsigned)ih, (unsigned)p.IW) +
-          (unsigned)iw;
-      const uint32_t off = ok ? __umul24(pix, (unsigned)cstride) + (uint32_t)(x_ci[j] * 2)
-                              : p.x_bytes;
-      dma16_opaque(rx, Xs + buf * SR * BKK + (j * NL + w4) * RPX * BKK, off);
-      int ow = xow[j] + dow, oh = xoh[j] + doh, n = xn[j] + dn;
-      if (ow >= p.OW) { ow -= p.OW; ++oh; }
-      if (oh >= p.OH) { oh -= p.OH; ++n; }
-      xow[j] = ow; xoh[j] = oh; xn[j] = n;
-    }
-  };
-  // group 0: wait until step `next` landed, with the steps after it (up to NST - 2) in flight
-  auto wait_step = [&](int next) {
-    const int ahead = min(NST - 2, nit - 1 - next);
-    if (ahead >= NST - 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (NST - 2)) : "memory");
-    else if (NST > 3 && ahead == 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * 2) : "memory");
-    else if (ahead == 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
-  typename WMfma<MF>::acc_t acc[TCO / MF][TKK / MF];
-#pragma unroll
-  for (int i = 0; i < TCO / MF; ++i)
-#pragma unroll
-    for (int j = 0; j < TKK / MF; ++j) acc[i][j] = {};
-  WgFrags<TCO, TKK, BCO, BKK, MF> fr;
-
-  if (grp == 0) {
-#pragma unroll
-    for (int j = 0; j < NST - 1; ++j)
-      if (j < nit) issue(j, j);
-    if (nit > 0) wait_step(0);
-  }
-  WG_PHASE_BARRIER();
-  int cur = 0;
-  for (int s = 0; s < nit; ++s) {
-    // phase A
-    if (grp == 0) {
-      if (s + NST - 1 < nit) issue(s + NST - 1, cur == 0 ? NST - 1 : cur - 1);
-      wg_read32<TCO, TKK, BCO, BKK, MF>(Ds + cur * SR * BCO, Xs + cur * SR * BKK, co_w, kk_w, fr);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    } else if (s > 0) {
-      __builtin_amdgcn_s_setprio(1);
-      wg_mfma32<TCO, TKK, BCO, BKK, MF>(fr, acc);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    WG_PHASE_BARRIER();
-    // phase B
-    if (grp == 0) {
-      __builtin_amdgcn_s_setprio(1);
-      wg_mfma32<TCO, TKK, BCO, BKK, MF>(fr, acc);
-      __builtin_amdgcn_s_setprio(0);
-      if (s + 1 < nit) wait_step(s + 1);
-    } else {
-      wg_read32<TCO, TKK, BCO, BKK, MF>(Ds + cur * SR * BCO, Xs + cur * SR * BKK, co_w, kk_w, fr);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    WG_PHASE_BARRIER();
-    cur = cur + 1 == NST ? 0 : cur + 1;
-  }
-  if (grp == 1 && nit > 0) wg_mfma32<TCO, TKK, BCO, BKK, MF>(fr, acc);
-  wgrad_store_at<TCO, TKK, MF>(p, acc, split, co0 + co_w, k0 + kk_w);
-}
-
 // Weight gradient of a 3x3 / stride-1 / pad-1 convolution (16x16 / 32x32, C in {64, 128}) with
 // the input patch reuse of igemm_patch: a block owns a (64 output channels, 64 input channels)
 // tile of all 9 taps and walks its share of 256-pixel spatial tiles; per tile the dY rows and
@@ -2653,29 +2418,14 @@ void launch_wgrad_pipe(const WgradArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
-// PRO_OK false: the X-operand prologue is not instantiated (it spills; wgrad_variant_ok rejects it)
-template <int BCO, int BKK, int MF, int NST>
-void launch_wgrad_pp(const WgradArgs& a0, hipStream_t s) {
-  WgradArgs a = a0;
-  a.nCo = (a.N + BCO - 1) / BCO;
-  a.nKk = (a.K + BKK - 1) / BKK;
-  const int grid = a.nCo * a.nKk * a.splits;
-  const size_t lds = (size_t)NST * 32 * (BCO + BKK) * 2;
-  hipLaunchKernelGGL((wgrad_pp<BCO, BKK, MF, NST>), dim3(grid), dim3(512), lds, s, a);
-  HIP_CHECK_LAUNCH();
-}
-
-template <int BCO, int BKK, int WM, int WN, int NST = 2, int MF = 16, bool PRO_OK = true>
+template <int BCO, int BKK, int WM, int WN, int NST = 2, int MF = 16>
 void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   a.nCo = (a.N + BCO - 1) / BCO;
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
   const size_t lds = (size_t)NST * 64 * (BCO + BKK) * 2 + (a.pro_sc != nullptr ? 16 * BKK : 0);
-  if constexpr (!PRO_OK)
-    hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, false, NST, MF>), dim3(grid),
-                       dim3(64 * WM * WN), lds, s, a);
-  else if (a.pro_sc != nullptr)
+  if (a.pro_sc != nullptr)
     hipLaunchKernelGGL((wgrad_glds<BCO, BKK, WM, WN, true, NST, MF>), dim3(grid), dim3(64 * WM * WN),
                        lds, s, a);
   else
@@ -2716,10 +2466,7 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {256, 128, 256}, {64, 64, 256},
                                   {64, 128, 768}, {128, 64, 768},
                                   {256, 256, 256}, {256, 128, 256}, {128, 256, 256},
-                                  {256, 256, 256}, {256, 128, 256}, {128, 256, 256},
-                                  {256, 256, 256}, {256, 256, 256}, {256, 256, 256},
-                                  {128, 128, 512}, {128, 256, 256}, {256, 128, 256},
-                                  {256, 256, 256}, {128, 256, 256}, {256, 128, 256}};
+                                  {256, 256, 256}};
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 // wgrad_tn with loads two steps ahead (DEEP): the 64 x 128 / 128 x 64 tiles gain 10-17 % on the
@@ -2728,18 +2475,10 @@ constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one i
 constexpr int WG_DEEP0 = 18;
 // 20-22: wgrad_pipe (32-row steps, 4-5 LDS stages with all but one in flight), no prologues
 constexpr int WG_PIPE0 = 20;
-// 23-27: wgrad_glds on v_mfma_f32_32x32x16_bf16 (23-25: the 8-wave / 4-wave tiles of 9, 7, 8;
-// 27: 4 waves of 128 x 128) and 26: 4 waves of 128 x 128 on 16x16x32 — the 128 x 128 wave tile
-// reads 2/3 of the LDS fragment bytes per FLOP of a 128 x 64 one; X-operand prologue allowed
-// (not on 26: it spills there)
+// 23: wgrad_glds 256 x 256 (8 waves) on v_mfma_f32_32x32x16_bf16 (as 9): half the MFMA and
+// ~17 % fewer VALU instructions, 1-4 % faster on the layer3 / layer4 3x3 weight gradients; the
+// other 32x32x16 tiles and the ping-pong kernel were measured and removed (r4 optimisation log)
 constexpr int WG_GLDS32 = 23;
-// 28, 30, 31: wgrad_pipe 256 x 256 / 128 x 256 / 256 x 128 (8 waves) on 32x32x16 (as 20, 22, 21)
-constexpr int WG_PIPE32 = 28;
-// 29: wgrad_glds 128 x 128 (4 waves) on 32x32x16 (as 6), X-operand prologue allowed
-constexpr int WG_GLDS32B = 29;
-// 32-34: wgrad_pp (two wave groups trading read / MFMA phases), 16x16x32, tiles 256 x 256,
-// 128 x 256, 256 x 128 (the 32x32x16 form spills there); no prologues
-constexpr int WG_PP0 = 32;
 
 
 // -------------------------------------------------- fused 1x1 backward: dgrad + wgrad in one pass
@@ -3108,8 +2847,7 @@ bool wgrad_variant_glds(int v) { return (v >= WG_GLDS0 && v < WG_PATCH0) || v >=
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
   if (v == WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);
-  if ((v >= WG_GLDS32 && v < WG_PIPE32) || v == WG_GLDS32B)
-    return !dy_pro && !(pro && v == WG_GLDS32 + 3) && igemm_glds_ok(g, pro, false);
+  if (v == WG_GLDS32) return !dy_pro && igemm_glds_ok(g, pro, false);
   if (v >= WG_PIPE0) return !dy_pro && !pro && igemm_glds_ok(g, false, false);
   if (v >= WG_DEEP0) return true;  // register-staged: every prologue
   // wgrad_glds has the X-operand BN-apply prologue only (no dY BN-backward prologue)
@@ -3218,17 +2956,6 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 21: launch_wgrad_pipe<256, 128, 4, 2, 32, 5>(a, s); break;
     case 22: launch_wgrad_pipe<128, 256, 2, 4, 32, 5>(a, s); break;
     case 23: launch_wgrad_glds<256, 256, 2, 4, 2, 32>(a, s); break;
-    case 24: launch_wgrad_glds<256, 128, 2, 2, 2, 32>(a, s); break;
-    case 25: launch_wgrad_glds<128, 256, 2, 2, 2, 32>(a, s); break;
-    case 26: launch_wgrad_glds<256, 256, 2, 2, 2, 16, false>(a, s); break;
-    case 27: launch_wgrad_glds<256, 256, 2, 2, 2, 32>(a, s); break;
-    case 28: launch_wgrad_pipe<256, 256, 2, 4, 32, 4, 32>(a, s); break;
-    case 29: launch_wgrad_glds<128, 128, 2, 2, 2, 32>(a, s); break;
-    case 30: launch_wgrad_pipe<128, 256, 2, 4, 32, 5, 32>(a, s); break;
-    case 31: launch_wgrad_pipe<256, 128, 4, 2, 32, 5, 32>(a, s); break;
-    case 32: launch_wgrad_pp<256, 256, 16, 4>(a, s); break;
-    case 33: launch_wgrad_pp<128, 256, 16, 4>(a, s); break;
-    case 34: launch_wgrad_pp<256, 128, 16, 4>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;

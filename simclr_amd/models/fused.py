@@ -147,6 +147,11 @@ class FusedStages:
         self._bnb_max_cin = 128
         # BN1's backward in conv1's operand prologues as well: measured +0.85 ms/step (r4 log)
         self.lazy_bn1 = False
+        # a downsample block's output gradient: BN3's backward in conv3's operand prologues and
+        # only the downsample BN's gradient materialised (one-output apply instead of the
+        # two-output bn_bwd_apply2), where conv3 takes the prologue (_bnb_ok)
+        self.lazy_bn3_ds = os.environ.get("SIMCLR_AB_LAZY3DS", "0") != "0"
+        self._lazy_bn3_ds_dual_only = os.environ.get("SIMCLR_AB_LAZY3DS", "1") != "2"
         # weight gradients on a second stream (forked after each conv's dY is final, joined at
         # the end of the backward): they only feed the flat gradient buffer, so they overlap the
         # dgrad / BatchNorm chain that the next layer's gradient depends on
@@ -447,6 +452,15 @@ class FusedStages:
         M = a.numel() // a.shape[-1]
         return (self.bnb_prologue and cs.k == 1 and cs.stride == 1 and M % S == 0
                 and (M // S) % 256 == 0 and cs.conv.in_channels <= getattr(self, "_bnb_max_cin", 128))
+
+    def _lazy_bn3_ds_ok(self, b: _BlockSpec, tp: _BlockTape, aL: torch.Tensor, S: int) -> bool:
+        L = len(b.convs) - 1
+        if not (getattr(self, "lazy_bn3_ds", False) and L > 0 and self._bnb_ok(b.convs[L], aL, S)):
+            return False
+        if not getattr(self, "_lazy_bn3_ds_dual_only", True):
+            return True
+        xin, pro_ss = tp.ins[L]
+        return self._bwd1x1_ok(b.convs[L], aL, xin, pro_ss, tp.acts[L - 1], S)
 
     def _lazy_bn1_ok(self, b: _BlockSpec, a1: torch.Tensor, S: int) -> bool:
         """BN1's backward applied in conv1's dgrad / weight-gradient operand prologues instead
@@ -804,9 +818,14 @@ class FusedStages:
             dad = torch.empty_like(tp.ad)
             if pre is not None and hd is not None:
                 # both BNs of the block output from one pass over g3 (their partials came
-                # from the following block's dgrad epilogue)
+                # from the following block's dgrad epilogue) — or only the downsample BN's,
+                # with BN3's backward left to conv3's operand prologues
                 coefd = self._bn_bwd_finish(ops, hd, S)
-                ops.bn_bwd_apply2(g3, aL, coefL, da, tp.ad, coefd, dad, S)
+                if self._lazy_bn3_ds_ok(b, tp, aL, S):
+                    lazy = (aL, coefL)
+                    ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
+                else:
+                    ops.bn_bwd_apply2(g3, aL, coefL, da, tp.ad, coefd, dad, S)
             else:
                 nblk_d = ops.bn_blocks(R, C, S)
                 partial_d = torch.empty((S * nblk_d * 2 * C,), device=dev, dtype=torch.float32)
