@@ -149,9 +149,11 @@ class FusedStages:
         self.lazy_bn1 = False
         # a downsample block's output gradient: BN3's backward in conv3's operand prologues and
         # only the downsample BN's gradient materialised (one-output apply instead of the
-        # two-output bn_bwd_apply2), where conv3 takes the prologue (_bnb_ok)
-        self.lazy_bn3_ds = os.environ.get("SIMCLR_AB_LAZY3DS", "0") != "0"
-        self._lazy_bn3_ds_dual_only = os.environ.get("SIMCLR_AB_LAZY3DS", "1") != "2"
+        # two-output bn_bwd_apply2) where conv3's backward is the fused 1x1 kernel (layer1.0):
+        # -0.12 ms/step (3 of 3 A/B rounds); also on the other prologue-eligible conv3s
+        # (layer2.0, register-staged weight gradient) neutral to worse (r4 optimisation log)
+        self.lazy_bn3_ds = True
+        self._lazy_bn3_ds_dual_only = True
         # weight gradients on a second stream (forked after each conv's dY is final, joined at
         # the end of the backward): they only feed the flat gradient buffer, so they overlap the
         # dgrad / BatchNorm chain that the next layer's gradient depends on
