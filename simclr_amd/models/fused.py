@@ -767,8 +767,13 @@ class FusedStages:
             prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else None
             g, pre = self._block_backward(ops, st, S, self.blocks[idx], tapes[idx], g, pre, prev)
         if main is not None:
-            main.wait_stream(self._side)  # join: every weight gradient is in the flat buffer
-            self._side_keep.clear()
+            if store is not None and getattr(store, "defer_side_join", False):
+                # joined in store.finish(), after the stem's backward
+                keep, self._side_keep = self._side_keep, []
+                store.defer_join(self._side, keep)
+            else:
+                main.wait_stream(self._side)  # join: every weight gradient is in the flat buffer
+                self._side_keep.clear()
         self._wt_ready = False  # the optimizer step changes the weights
         return g
 

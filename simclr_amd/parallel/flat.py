@@ -98,6 +98,12 @@ class FlatParamStore:
         # a bucket's all-reduce waits for all of them
         self.producer_streams: List = []
         self._works: List = []
+        # defer_side_join (set by the trainers, which always call finish() before reading the
+        # gradients): the fused executor hands its weight-gradient stream's join to finish()
+        # instead of joining at the end of its own backward, so the stem's backward (autograd,
+        # after the executor) overlaps the tail of the weight gradients
+        self.defer_side_join = False
+        self._joins: List = []
         self.reset_step()
 
     # ------------------------------------------------------------------ parameters
@@ -192,8 +198,21 @@ class FlatParamStore:
         else:
             self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
 
+    def defer_join(self, stream, keep: List) -> None:
+        """The compute stream joins ``stream`` in finish(); ``keep`` holds the tensors that
+        stream still reads (released only after the join, so the caching allocator cannot hand
+        their memory to a compute-stream allocation while they are in use)."""
+        self._joins.append((stream, keep))
+
     def finish(self) -> None:
-        """Flush unlaunched buckets (unused params), then make the compute stream wait."""
+        """Join deferred producer streams, flush unlaunched buckets (unused params), then make
+        the compute stream wait for the all-reduces."""
+        if self._joins:
+            cur = torch.cuda.current_stream(self.grad.device)
+            for stream, keep in self._joins:
+                cur.wait_stream(stream)
+                keep.clear()
+            self._joins = []
         if not self.comm:
             return
         while self._next_launch < len(self.buckets):

@@ -73,6 +73,7 @@ class Trainer:
         prec = precision or cfg_get(cfg, "runtime.precision", "bf16")
         self.precision = prec if self.device.type == "cuda" else "fp32"
         self.model, self.store = build_contrastive_model(cfg, self.device, self.precision)
+        self.store.defer_side_join = True  # _step_body calls store.finish() before the optimizer
         batches = cfg["experiment"]["batches"]
         world = st.world_size
         # reference: int(num_samples / (batches * world)) (main.py:76)

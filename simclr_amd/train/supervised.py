@@ -93,6 +93,7 @@ def supervised(cfg) -> dict:
                            else None, bucket_mb=cfg_get(cfg, "runtime.bucket_mb", 32.0),
                            last_bucket_mb=cfg_get(cfg, "runtime.last_bucket_mb", 2.0))
     store.broadcast_from(0)
+    store.defer_side_join = True  # every step ends with store.finish() before the optimizer
     steps_per_epoch = max(1, int(len(train_ds) / (bs * st.world_size)))
     epochs = cfg["parameter"]["epochs"]
     total, warm = epochs * steps_per_epoch, cfg["parameter"]["warmup_epochs"] * steps_per_epoch
