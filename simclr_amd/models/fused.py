@@ -147,6 +147,9 @@ class FusedStages:
         self._bnb_max_cin = 128
         # BN1's backward in conv1's operand prologues as well: measured +0.85 ms/step (r4 log)
         self.lazy_bn1 = False
+        # expansion convs from this many input channels on read a materialised BN2+ReLU input
+        # (_mat_expand)
+        self.mat_expand_min_cin = 128
         # a downsample block's output gradient: BN3's backward in conv3's operand prologues and
         # only the downsample BN's gradient materialised (one-output apply instead of the
         # two-output bn_bwd_apply2) where conv3's backward is the fused 1x1 kernel (layer1.0):
@@ -455,6 +458,17 @@ class FusedStages:
         return (self.bnb_prologue and cs.k == 1 and cs.stride == 1 and M % S == 0
                 and (M // S) % 256 == 0 and cs.conv.in_channels <= getattr(self, "_bnb_max_cin", 128))
 
+    def _mat_expand(self, cs: _ConvSpec) -> bool:
+        """A bottleneck's expansion 1x1 conv (conv3, Co = 4 Ci) takes its input BN2+ReLU as a
+        materialised tensor instead of in its operand prologue from ``mat_expand_min_cin`` input
+        channels on: the short-K GEMM re-reads and re-transforms its A tile once per output
+        column tile (34-46 % of its roofline, r4 per-op table), and the backward's weight gradient
+        then reads the stored input with the LDS-DMA tiles instead of an X-operand prologue.
+        Below that (layer1, Ci = 64) conv3's backward is the fused 1x1 kernel, which applies
+        BN2 itself.  -0.3 ms/step (r4 optimisation log)."""
+        cin, cout = cs.conv.in_channels, cs.conv.out_channels
+        return cs.k == 1 and cout >= 4 * cin and cin >= self.mat_expand_min_cin
+
     def _lazy_bn3_ds_ok(self, b: _BlockSpec, tp: _BlockTape, aL: torch.Tensor, S: int) -> bool:
         L = len(b.convs) - 1
         if not (getattr(self, "lazy_bn3_ds", False) and L > 0 and self._bnb_ok(b.convs[L], aL, S)):
@@ -687,10 +701,11 @@ class FusedStages:
                 forked = True
             for ci_, cs in enumerate(b.convs):
                 _ext.TAG = f"{b.name} conv{ci_ + 1} fwd"
-                if pro_ss is not None and cs.k > 1:
+                if pro_ss is not None and (cs.k > 1 or self._mat_expand(cs)):
                     # a k x k conv re-gathers every input pixel k² times: applying BN+ReLU in
                     # its prologue costs more VALU work than one materialising pass (measured,
-                    # also for the LDS-resident patch kernels: r3 optimisation log)
+                    # also for the LDS-resident patch kernels: r3 optimisation log); likewise
+                    # the short-K expansion convs (_mat_expand)
                     bmat = torch.empty_like(cur)
                     ops.bn_apply_ss(cur, pro_ss, None, None, bmat, S, True)
                     cur, pro_ss = bmat, None
