@@ -1757,6 +1757,206 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_glds(WgradArgs p) {
   wgrad_store<BCO, BKK, WM, WN, MF>(p, acc, split, co0, k0);
 }
 
+// Weight-gradient fragments of one k sub-step (32 rows at MF 16, 16 rows at MF 32) of one wave
+template <int TCO, int TKK, int MF>
+struct WgKs {
+  bf16x8 a[TCO / MF], b[TKK / MF];
+};
+
+template <int SD, int SX, int TCO, int TKK, int MF>
+__device__ __forceinline__ void wg_read_ks(const uint16_t* Db, const uint16_t* Xb, int ks, int co_w,
+                                           int kk_w, WgKs<TCO, TKK, MF>& f) {
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  // rows / columns as in wgrad_mma (ks counts 32-row sub-steps at MF 16, 16-row ones at MF 32)
+  const int r1 = MF == 16 ? ks * 32 + 8 * g + q : ks * 16 + 8 * (g >> 1) + q;
+  const int cg = MF == 16 ? 4 * pp : 16 * (g & 1) + 4 * pp;
+#pragma unroll
+  for (int fm = 0; fm < TCO / MF; ++fm) {
+    const int col = co_w + fm * MF + cg;
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(i16x4, Db + r1 * SD + (wg_swz<SD, MF>(r1, col))));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(i16x4, Db + (r1 + 4) * SD + (wg_swz<SD, MF>(r1 + 4, col))));
+    i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    f.a[fm] = __builtin_bit_cast(bf16x8, v);
+  }
+#pragma unroll
+  for (int fn = 0; fn < TKK / MF; ++fn) {
+    const int col = kk_w + fn * MF + cg;
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(i16x4, Xb + r1 * SX + (wg_swz<SX, MF>(r1, col))));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(i16x4, Xb + (r1 + 4) * SX + (wg_swz<SX, MF>(r1 + 4, col))));
+    i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    f.b[fn] = __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int TCO, int TKK, int MF>
+__device__ __forceinline__ void wg_mma_ks(const WgKs<TCO, TKK, MF>& f,
+                                          typename WMfma<MF>::acc_t (&acc)[TCO / MF][TKK / MF]) {
+#pragma unroll
+  for (int fm = 0; fm < TCO / MF; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < TKK / MF; ++fn) {
+      if constexpr (MF == 16)
+        acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[fm], f.b[fn], acc[fm][fn], 0, 0, 0);
+      else
+        acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[fm], f.b[fn], acc[fm][fn], 0, 0, 0);
+    }
+}
+
+// LDS-DMA weight gradient with the fragment reads carried across the barrier (no operand
+// prologues).  In wgrad_glds every wave starts a step with its fragment reads right after the
+// barrier, so all waves of the CU wait on LDS together while the MFMA pipes idle (the compute half
+// alone ran at ~55 % of the MFMA rate, r4 log).  Here the fragments roll through two register
+// sets: sub-step j + 1 (one MFMA k-step) is read while sub-step j multiplies, and the last
+// sub-step of step it multiplies after the barrier, under the reads of step it + 1's first
+// sub-step — reads are always in flight under MFMAs, and only two sub-steps of fragments are
+// live (the 256 x 256 tile fits without spilling).  The barrier also frees the step's buffer:
+// the DMA of step it + 2 is issued right after it (2 LDS stages, one step of DMA in flight, as
+// wgrad_glds).
+template <int BCO, int BKK, int WM, int WN, int MF>
+__global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_xp(WgradArgs p) {
+  constexpr int NW = WM * WN;
+  constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = 64 / (RPD * NW);
+  constexpr int CPX = BKK / 8, RPX = 64 / CPX, XI = 64 / (RPX * NW);
+  static_assert(DI >= 1 && XI >= 1 && DI * RPD * NW == 64 && XI * RPX * NW == 64, "wgrad xp");
+  constexpr int PER = DI + XI;
+  constexpr int TCO = BCO / WM, TKK = BKK / WN;
+  constexpr int NSUB = MF == 16 ? 2 : 4;  // k sub-steps per 64-row step (even: f[0] restarts)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ds = (uint16_t*)smem;       // [2][64][BCO]
+  uint16_t* Xs = Ds + 2 * 64 * BCO;     // [2][64][BKK]
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int co_w = (wid / WN) * TCO, kk_w = (wid % WN) * TKK;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = p.nCo * p.nKk;
+  const int split = lbid / tiles;
+  const int tile = lbid % tiles;
+  const int co0 = (tile / p.nKk) * BCO;
+  const int k0 = (tile % p.nKk) * BKK;
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, (int)p.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, (int)p.x_bytes, 0x00020000);
+  const int mbeg = split * p.iters_per_split * 64;
+  const int mend_raw = mbeg + p.iters_per_split * 64;
+  const int mend = mend_raw < p.M ? mend_raw : p.M;
+  const int nit = mend > mbeg ? (mend - mbeg + 63) / 64 : 0;
+  const int OHW = p.OH * p.OW;
+
+  int d_row[DI];
+  uint32_t d_off[DI];
+  bool d_cok[DI];
+#pragma unroll
+  for (int j = 0; j < DI; ++j) {
+    const int r = (j * NW + wid) * RPD + lane / CPD;
+    const int col = co0 + wg_swz<BCO, MF>(r, (lane % CPD) * 8);
+    d_row[j] = r;
+    d_cok[j] = col < p.N;
+    d_off[j] = (uint32_t)(((size_t)(mbeg + r) * p.N + col) * 2);
+  }
+  const uint32_t dstep = (uint32_t)(64 * p.N * 2);
+  int x_row[XI], x_ci[XI], x_ihb[XI], x_iwb[XI], xn[XI], xoh[XI], xow[XI];
+  bool x_kok[XI];
+#pragma unroll
+  for (int j = 0; j < XI; ++j) {
+    const int r = (j * NW + wid) * RPX + lane / CPX;
+    const int kk = k0 + wg_swz<BKK, MF>(r, (lane % CPX) * 8);
+    x_row[j] = r;
+    x_kok[j] = kk < p.K;
+    const int tap = x_kok[j] ? kk / p.C : 0;
+    x_ci[j] = kk - tap * p.C;
+    const int kh = tap / p.KW, kw = tap - (tap / p.KW) * p.KW;
+    x_ihb[j] = p.ih0 + kh * p.dh;
+    x_iwb[j] = p.iw0 + kw * p.dw;
+    const int m = mbeg + r;
+    xn[j] = m / OHW;
+    const int rem = m - xn[j] * OHW;
+    xoh[j] = rem / p.OW;
+    xow[j] = rem - xoh[j] * p.OW;
+  }
+  const int dn = 64 / OHW, dr = 64 - dn * OHW;
+  const int doh = dr / p.OW, dow = dr - doh * p.OW;
+  const int cstride = p.C * 2;
+
+  auto issue = [&](int it, int buf) {
+    const int mb = mbeg + it * 64;
+#pragma unroll
+    for (int j = 0; j < DI; ++j) {
+      const bool ok = mb + d_row[j] < mend && d_cok[j];
+      dma16_opaque(rd, Ds + buf * 64 * BCO + (j * NW + wid) * RPD * BCO,
+                   ok ? d_off[j] : p.dy_bytes);
+      d_off[j] += dstep;
+    }
+#pragma unroll
+    for (int j = 0; j < XI; ++j) {
+      const int ih = (int)__umul24((unsigned)xoh[j], (unsigned)p.ish) + x_ihb[j];
+      const int iw = (int)__umul24((unsigned)xow[j], (unsigned)p.isw) + x_iwb[j];
+      const bool ok = mb + x_row[j] < mend && x_kok[j] && (unsigned)ih < (unsigned)p.IH &&
+                      (unsigned)iw < (unsigned)p.IW;
+      const uint32_t pix =
+          __umul24(__umul24((unsigned)xn[j], (unsigned)p.IH) + (unsigned)ih, (unsigned)p.IW) +
+          (unsigned)iw;
+      const uint32_t off = ok ? __umul24(pix, (unsigned)cstride) + (uint32_t)(x_ci[j] * 2)
+                              : p.x_bytes;
+      dma16_opaque(rx, Xs + buf * 64 * BKK + (j * NW + wid) * RPX * BKK, off);
+      int ow = xow[j] + dow, oh = xoh[j] + doh, n = xn[j] + dn;
+      if (ow >= p.OW) { ow -= p.OW; ++oh; }
+      if (oh >= p.OH) { oh -= p.OH; ++n; }
+      xow[j] = ow; xoh[j] = oh; xn[j] = n;
+    }
+  };
+
+  typename WMfma<MF>::acc_t acc[TCO / MF][TKK / MF];
+#pragma unroll
+  for (int i = 0; i < TCO / MF; ++i)
+#pragma unroll
+    for (int j = 0; j < TKK / MF; ++j) acc[i][j] = {};
+  WgKs<TCO, TKK, MF> f[2];  // rolling pair: sub-step j + 1 is read while sub-step j multiplies
+
+  if (nit > 0) {
+    issue(0, 0);
+    if (nit > 1) {
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step 0 landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    wg_read_ks<BCO, BKK, TCO, TKK, MF>(Ds, Xs, 0, co_w, kk_w, f[0]);
+  }
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    const uint16_t* Db = Ds + cur * 64 * BCO;
+    const uint16_t* Xb = Xs + cur * 64 * BKK;
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      if (j + 1 < NSUB) {
+        wg_read_ks<BCO, BKK, TCO, TKK, MF>(Db, Xb, j + 1, co_w, kk_w, f[(j + 1) & 1]);
+      } else {
+        // this wave's reads of step it retired; step it + 1 landed (nothing else in flight).
+        // sched_barrier keeps the last sub-step's MFMAs below the barrier, under the next
+        // step's first reads
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave done with buffer cur; step it + 1 visible
+        __builtin_amdgcn_sched_barrier(0);
+        if (it + 2 < nit) issue(it + 2, cur);
+        if (it + 1 < nit)
+          wg_read_ks<BCO, BKK, TCO, TKK, MF>(Ds + (cur ^ 1) * 64 * BCO, Xs + (cur ^ 1) * 64 * BKK,
+                                             0, co_w, kk_w, f[0]);
+      }
+      wg_mma_ks<TCO, TKK, MF>(f[j & 1], acc);
+    }
+  }
+  wgrad_store_at<TCO, TKK, MF>(p, acc, split, co0 + co_w, k0 + kk_w);
+}
+
 // Deep-pipelined LDS-DMA weight gradient (no operand prologues).  wgrad_glds stages 64-row
 // steps in two LDS buffers: the DMA of step it+1 is issued at the top of step it and must land
 // within ONE step of MFMAs (~0.4-0.9 us for the big tiles) — less than an HBM / remote-L2 round
@@ -2418,6 +2618,17 @@ void launch_wgrad_pipe(const WgradArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+template <int BCO, int BKK, int WM, int WN, int MF>
+void launch_wgrad_xp(const WgradArgs& a0, hipStream_t s) {
+  WgradArgs a = a0;
+  a.nCo = (a.N + BCO - 1) / BCO;
+  a.nKk = (a.K + BKK - 1) / BKK;
+  const int grid = a.nCo * a.nKk * a.splits;
+  const size_t lds = (size_t)2 * 64 * (BCO + BKK) * 2;
+  hipLaunchKernelGGL((wgrad_xp<BCO, BKK, WM, WN, MF>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
+  HIP_CHECK_LAUNCH();
+}
+
 template <int BCO, int BKK, int WM, int WN, int NST = 2, int MF = 16>
 void launch_wgrad_glds(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
@@ -2466,7 +2677,8 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {256, 128, 256}, {64, 64, 256},
                                   {64, 128, 768}, {128, 64, 768},
                                   {256, 256, 256}, {256, 128, 256}, {128, 256, 256},
-                                  {256, 256, 256}};
+                                  {256, 256, 256},
+                                  {256, 256, 256}, {256, 128, 256}, {128, 128, 512}};
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 // wgrad_tn with loads two steps ahead (DEEP): the 64 x 128 / 128 x 64 tiles gain 10-17 % on the
@@ -2479,6 +2691,9 @@ constexpr int WG_PIPE0 = 20;
 // ~17 % fewer VALU instructions, 1-4 % faster on the layer3 / layer4 3x3 weight gradients; the
 // other 32x32x16 tiles and the ping-pong kernel were measured and removed (r4 optimisation log)
 constexpr int WG_GLDS32 = 23;
+// 24-26: wgrad_xp (fragment reads carried across the barrier, no prologues) on 32x32x16:
+// 256 x 256 / 256 x 128 (8 waves), 128 x 128 (4 waves)
+constexpr int WG_XP0 = 24;
 
 
 // -------------------------------------------------- fused 1x1 backward: dgrad + wgrad in one pass
@@ -2956,6 +3171,9 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 21: launch_wgrad_pipe<256, 128, 4, 2, 32, 5>(a, s); break;
     case 22: launch_wgrad_pipe<128, 256, 2, 4, 32, 5>(a, s); break;
     case 23: launch_wgrad_glds<256, 256, 2, 4, 2, 32>(a, s); break;
+    case 24: launch_wgrad_xp<256, 256, 2, 4, 32>(a, s); break;
+    case 25: launch_wgrad_xp<256, 128, 4, 2, 32>(a, s); break;
+    case 26: launch_wgrad_xp<128, 128, 2, 2, 32>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;
