@@ -67,7 +67,8 @@ def drains(lines):
     for i, ln in enumerate(lines):
         if DMA.search(ln):
             pending, wait_at = True, None
-        elif "s_barrier" in ln:
+        elif "s_barrier" in ln or re.match(r"\s*s_branch\s", ln):
+            # (an unconditional branch: the next line in layout order is not its successor)
             pending, wait_at = False, None
         elif pending and WAIT_VM.search(ln):
             wait_at = i
