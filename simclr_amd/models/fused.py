@@ -657,6 +657,25 @@ class FusedStages:
         ops.weight_transform_batch(self._wt_table[0], self._wt_table[1])
         self._wt_ready = True
 
+    def _prefetch_dgrad_weights(self, ops, xn: torch.Tensor) -> None:
+        """The batched dgrad-weight transform (prepare_backward) depends only on the weights, which
+        are final once the previous optimizer step ran: issue it on the (idle during the forward)
+        weight-gradient stream at the start of the forward, so it is off the critical path of
+        the backward, which waits on its event."""
+        self._wt_event = None
+        if not (self.wgrad_stream and xn.is_cuda):
+            return
+        dev = xn.device
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(device=dev)
+        self._side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self._side):
+            self.prepare_backward(ops)
+        if self._wt_ready:
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+            self._wt_event = ev
+
     def _dgrad_weight(self, ops, cs: _ConvSpec, w, key, p):
         if getattr(self, "_wt_ready", False):
             wt = self._wt_cache.get((id(cs.conv), key))
@@ -674,6 +693,7 @@ class FusedStages:
         self.calls += 1
         tapes: List[_BlockTape] = []
         x = xn
+        self._prefetch_dgrad_weights(ops, xn)
         br = self._branch_stream(xn)
         pend = None  # the previous block's output, not yet formed: (aL, ss, res, rss, out, mask)
         for b in self.blocks:
@@ -768,7 +788,12 @@ class FusedStages:
         ops = _ext.ops()
         st = pstate.get()
         S = self.S
-        self.prepare_backward(ops)
+        ev = getattr(self, "_wt_event", None)
+        if ev is not None and self._wt_ready:
+            torch.cuda.current_stream(gout.device).wait_event(ev)  # transposed during the forward
+        else:
+            self.prepare_backward(ops)
+        self._wt_event = None
         main = None
         if self.wgrad_stream and gout.is_cuda:
             main = torch.cuda.current_stream(gout.device)
