@@ -75,15 +75,21 @@ __global__ __launch_bounds__(LARS_THREADS) void k_lars_update(
     const float* __restrict__ seg_wd, const int* __restrict__ seg_flags,
     const float* __restrict__ norms, const float* __restrict__ lr_ptr, float momentum, float trust,
     float eps, float grad_scale, int nesterov) {
+  __shared__ float red[LARS_THREADS / 64 + 1];
   const int c = blockIdx.x;
   const int seg = chunk_seg[c];
   const float wd = seg_wd[seg];
   const int flags = seg_flags[seg];
+  // the segment's chunk slots summed by the whole block (fixed slot -> thread assignment and
+  // reduction tree: deterministic); one thread walking them serially cost up to ~250 dependent
+  // loads per block on the big 3x3 / head tensors
   float sp = 0.f, sg = 0.f;
-  for (int k = seg_chunk_beg[seg]; k < seg_chunk_end[seg]; ++k) {
+  for (int k = seg_chunk_beg[seg] + threadIdx.x; k < seg_chunk_end[seg]; k += LARS_THREADS) {
     sp += norms[2 * k];
     sg += norms[2 * k + 1];
   }
+  sp = block_sum(sp, red);
+  sg = block_sum(sg, red);
   const float pn = sqrtf(sp), gn = sqrtf(sg);
   // Apex LARC: only when both norms are non-zero is wd folded and the grad rescaled
   float scale = grad_scale, wdf = 0.f;
@@ -99,13 +105,33 @@ __global__ __launch_bounds__(LARS_THREADS) void k_lars_update(
   const float lr = lr_ptr[0];
   const int beg = chunk_beg[c], end = chunk_end[c];
   const bool write_shadow = (flags & 2) && shadow != nullptr;
-  for (int i = beg + threadIdx.x; i < end; i += LARS_THREADS) {
-    const float pv = p[i];
-    const float d = g[i] * scale + wdf * pv;
-    const float b = momentum * mom[i] + d;  // mom starts at 0 == torch's buf=clone(d)
-    mom[i] = b;
+  auto step1 = [&](float pv, float gv, float mv, float& bo) {
+    const float d = gv * scale + wdf * pv;
+    const float b = momentum * mv + d;  // mom starts at 0 == torch's buf=clone(d)
+    bo = b;
     const float upd = nesterov ? d + momentum * b : b;
-    const float np = pv - lr * upd;
+    return pv - lr * upd;
+  };
+  // 16-byte accesses (chunk starts are 64-element aligned; only a segment's end may not be a
+  // multiple of 4: that tail of < 4 elements is reached by one thread)
+  int i = beg + threadIdx.x * 4;
+  for (; i + 3 < end; i += LARS_THREADS * 4) {
+    const float4 pv = *(const float4*)(p + i);
+    const float4 gv = *(const float4*)(g + i);
+    const float4 mv = *(const float4*)(mom + i);
+    float4 b, np;
+    np.x = step1(pv.x, gv.x, mv.x, b.x);
+    np.y = step1(pv.y, gv.y, mv.y, b.y);
+    np.z = step1(pv.z, gv.z, mv.z, b.z);
+    np.w = step1(pv.w, gv.w, mv.w, b.w);
+    *(float4*)(mom + i) = b;
+    *(float4*)(p + i) = np;
+    if (write_shadow) *(u32x2*)(shadow + i) = (u32x2){pack2bf(np.x, np.y), pack2bf(np.z, np.w)};
+  }
+  for (; i < end; ++i) {
+    float b;
+    const float np = step1(p[i], g[i], mom[i], b);
+    mom[i] = b;
     p[i] = np;
     if (write_shadow) shadow[i] = f2bf(np);
   }
