@@ -46,9 +46,24 @@ __global__ __launch_bounds__(LARS_THREADS) void k_lars_norms(const float* __rest
   const int c = blockIdx.x;
   const int beg = chunk_beg[c], end = chunk_end[c];
   float sp = 0.f, sg = 0.f;
-  // beg/end are multiples of 4 except possibly the segment's end
+  // beg/end are multiples of 4 except possibly the segment's end; four 16-byte loads of each
+  // operand in flight per thread (one pair at a time ran at ~4 TB/s)
   int i = beg + threadIdx.x * 4;
-  for (; i + 3 < end; i += LARS_THREADS * 4) {
+  constexpr int ST = LARS_THREADS * 4;
+  for (; i + 3 * ST + 3 < end; i += 4 * ST) {
+    float4 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = *(const float4*)(p + i + u * ST);
+      b[u] = *(const float4*)(g + i + u * ST);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sp += a[u].x * a[u].x + a[u].y * a[u].y + a[u].z * a[u].z + a[u].w * a[u].w;
+      sg += b[u].x * b[u].x + b[u].y * b[u].y + b[u].z * b[u].z + b[u].w * b[u].w;
+    }
+  }
+  for (; i + 3 < end; i += ST) {
     const float4 a = *(const float4*)(p + i);
     const float4 b = *(const float4*)(g + i);
     sp += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
