@@ -65,6 +65,7 @@ def _build(dev, fused=True):
                 blk.bn3.weight.mul_(0.2)
     store = FlatParamStore(m, dev, shadow_dtype=torch.bfloat16, bucket_mb=4.0,
                            first_bucket_mb=1.0)
+    store.defer_side_join = True  # as the trainers: the weight-gradient stream joins in finish()
     m.train()
     return m, store
 
