@@ -56,7 +56,12 @@ def self_launch(args, argv) -> int:
     # visibility variables / KFD topology only: this parent forks every rank and must never
     # initialise HIP itself (torch.cuda.device_count() can fall back to hipGetDeviceCount)
     ndev = visible_gpu_count()
-    if ndev and ndev < args.gpus and os.environ.get("SIMCLR_DIST_BACKEND") != "gloo":
+    if ndev == 0:
+        # every GPU hidden by a visibility variable: the ranks run on the CPU over gloo (the CPU
+        # rehearsal of the driver contract), never silently on fewer GPUs
+        print(f"[bench] no GPU visible: the {args.gpus} ranks run on the CPU (gloo)",
+              file=sys.stderr, flush=True)
+    elif ndev is not None and ndev < args.gpus and os.environ.get("SIMCLR_DIST_BACKEND") != "gloo":
         raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} GPU(s) visible")
     la = parse_args(["--nproc_per_node", str(args.gpus), "--master_addr", "127.0.0.1",
                      "--master_port", str(_free_port()), "--use_env", str(Path(__file__).resolve()),
@@ -98,6 +103,18 @@ def _sync(dev, world):
         dist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+
+
+def _set_mode(tr, graph, mode: str) -> None:
+    """eager | graph (hipGraphLaunch) | streams (native multi-stream replay of the graph)."""
+    tr.graph = None if mode == "eager" else graph
+    tr.replay_mode = "streams" if mode == "streams" else "graph"
+
+
+def _exec_mode(tr) -> str:
+    if tr.graph is None:
+        return "eager"
+    return "streams" if (tr.replay_mode == "streams" and tr.sreplay is not None) else "graph"
 
 
 def run_ours(args, rank, world, dev):
@@ -195,25 +212,32 @@ def run_ours(args, rank, world, dev):
             tr.graph = None
             args.graph = False
     if auto and tr.graph is not None and t_eager is not None:
-        # execution-mode autotune: replaying the captured step vs issuing it eagerly (the HIP
-        # graph executor loses part of the side-stream overlap — 24.0 vs 23.4 ms/step at N=1 —
-        # while eager issue costs host time that grows with the ranks sharing the CPUs)
-        # PROBE_ROUNDS interleaved rounds of 2 eager + 2 replayed steps (box drift hits both
-        # arms alike); the slower rank decides, the same choice on every rank
-        g, t_graph = tr.graph, 0.0
+        # execution-mode autotune: eager issue vs replaying the captured step with the HIP graph
+        # executor vs the native multi-stream executor over the same captured nodes
+        # (runtime/graph_exec.py).  The HIP graph executor loses part of the side-stream overlap;
+        # eager issue costs host time that grows with the ranks sharing the CPUs.
+        # PROBE_ROUNDS interleaved rounds of 2 steps per arm (box drift hits every arm alike);
+        # the slower rank decides, the same choice on every rank
+        arms = ["eager", "graph"] + (["streams"] if tr.sreplay is not None else [])
+        g = tr.graph
+        tot = {a: 0.0 for a in arms}
         for _ in range(PROBE_ROUNDS):
-            tr.graph = None
-            t_eager += timed(2)
-            tr.graph = g
-            t_graph += timed(2)
+            for a in arms:
+                _set_mode(tr, g, a)
+                tot[a] += timed(2)
         n = 2 * PROBE_ROUNDS
-        tt = torch.tensor([t_eager, t_graph], dtype=torch.float64, device=dev)
+        tt = torch.tensor([tot[a] for a in arms], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        if float(tt[1]) >= float(tt[0]):
-            tr.graph = None
-        args.mode_probe_ms = [round(float(v) / n * 1000.0, 3) for v in tt.tolist()]
+        best = arms[int(torch.argmin(tt).item())]
+        _set_mode(tr, g, best)
+        args.mode_probe = {a: round(float(v) / n * 1000.0, 3) for a, v in zip(arms, tt.tolist())}
+        args.mode_probe_ms = [args.mode_probe["eager"], args.mode_probe["graph"]]
+    elif args.exec_mode in ("graph", "streams") and tr.graph is not None:
+        _set_mode(tr, tr.graph, "streams" if (args.exec_mode == "streams"
+                                              and tr.sreplay is not None) else "graph")
     args.graph = tr.graph is not None
+    args.exec_used = _exec_mode(tr)
     loss = None
 
     def measure():
@@ -250,7 +274,9 @@ def run_ours(args, rank, world, dev):
         args.graph = False
         args.bn_comm = "rccl(ipc-timeout, re-timed)"
         t0, t1 = measure()
-
+    args.exec_used = _exec_mode(tr)
+    if tr.sreplay is not None:
+        args.sreplay_stats = tr.sreplay.stats()
     return t1 - t0, float(loss.item()) if loss is not None else float("nan")
 
 
@@ -325,6 +351,10 @@ def main(argv=None):
                     help="capture the step in a hipGraph and replay it")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="issue every step eagerly (default: probe both, keep the faster)")
+    ap.add_argument("--exec", dest="exec_mode", default="auto",
+                    choices=["auto", "eager", "graph", "streams"],
+                    help="step issue mode: auto (probe eager / hipGraph / native multi-stream "
+                         "replay, keep the fastest), or one of them forced")
     ap.add_argument("--bucket-mb", dest="bucket_mb", type=float, default=32.0)
     ap.add_argument("--impl", choices=["ours", "reference"], default="ours")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -337,6 +367,10 @@ def main(argv=None):
                          "the flag disagree")
     if args.gather is None:
         args.gather = world > 1
+    if args.exec_mode == "eager":
+        args.graph = False
+    elif args.exec_mode in ("graph", "streams"):
+        args.graph = True
     if args.graph is None:
         # default: probe the eager step and the hipGraph replay of the whole step (RCCL
         # collectives included, thread-local capture mode) for 3 steps each and keep the faster
@@ -397,6 +431,9 @@ def main(argv=None):
             "impl": args.impl,
             "hip_graph": bool(args.graph and args.impl == "ours"),
             "exec_mode_probe_ms_eager_graph": getattr(args, "mode_probe_ms", None),
+            "exec_mode_probe_ms": getattr(args, "mode_probe", None),
+            "exec_mode": getattr(args, "exec_used", None),
+            "stream_replay": getattr(args, "sreplay_stats", None),
             "bn_stats_comm": args.bn_comm,
             "bn_comm_probe_ms_ipc_rccl": getattr(args, "comm_probe_ms", None),
             "host_issue_ms_per_step": (round(args.host_issue_ms, 3)

@@ -207,6 +207,12 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   }
   if (pro_d.has_value() && pro_d->defined()) {
     TORCH_CHECK(f.pro_sc, "igemm BN-backward prologue needs pro_sc (A) and pro_sh (B)");
+    // the BN-backward prologue + mode-4 epilogue is not instantiated for tiles above 256 x 128
+    // (the 256 x 256 tile with both fusions drains its DMA pipeline): conv.hip launch_glds
+    TORCH_CHECK(!(igemm_variant_glds((int)variant) && epi_mode == 4 &&
+                  igemm_variant_bm((int)variant) * igemm_variant_bn((int)variant) > 256 * 128),
+                "igemm: BN-backward prologue + mode-4 epilogue needs an LDS-DMA tile of at most "
+                "256 x 128 (variant ", variant, ")");
     TORCH_CHECK(pro_d->numel() >= (M / pro_seg_rows) * g.C, "igemm prologue: d [S][C] size");
     TORCH_CHECK(A2.has_value() && A2->numel() == A.numel(), "igemm prologue: A2 must match A");
     TORCH_CHECK(epi_mode == 0 || epi_mode == 3 || epi_mode == 4,

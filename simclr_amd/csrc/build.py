@@ -23,7 +23,7 @@ OUT = PKG / "_C.so"
 BUILD = HERE / "_build"
 KERNEL_SOURCES = ["conv.hip", "bn.hip", "misc.hip", "ntxent.hip", "lars.hip", "augment.hip",
                   "eval.hip", "comm.hip"]
-BINDINGS = ["bindings.cpp", "ipc.cpp"]  # the units that see the ATen headers
+BINDINGS = ["bindings.cpp", "ipc.cpp", "graphexec.cpp"]  # the units that see the ATen headers
 HEADERS = ["common.h", "kernels.h"]
 ARCH = os.environ.get("SIMCLR_OFFLOAD_ARCH", "gfx950")
 

@@ -2493,8 +2493,8 @@ void launch_glds(const IgemmArgs& a, hipStream_t s) {
       if (a.epi_mode == 3)
         launch_glds_t<BM, BN, WM, WN, 2, 3, NST>(a, s);
       else if (a.epi_mode == 4) {
-        // (the 256 x 256 tile with both fusions drains its DMA pipeline: not instantiated,
-        // igemm_bnb_epi4_ok rejects it)
+        // (the 256 x 256 tile with both fusions drains its DMA pipeline: not instantiated;
+        // the igemm binding rejects that combination before any launch)
         if constexpr (BM * BN <= 256 * 128) {
           if (a.stats2 != nullptr)
             launch_glds_t<BM, BN, WM, WN, 2, 5, NST>(a, s);

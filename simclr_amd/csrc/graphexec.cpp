@@ -1,0 +1,328 @@
+// Multi-stream replay of a captured hipGraph (the training step) from a native launch list.
+//
+// Why: the whole SimCLR step (augment → forward → NT-Xent → backward → LARS, ~500 kernels) can
+// be captured into one hipGraph, but the HIP graph executor runs it with less concurrency than
+// the eager schedule (the weight gradients on their side stream no longer overlap the
+// dgrad/BatchNorm chain: profiles/r4_optimization_log.md), while eager issue costs ~30 µs of
+// Python + dispatcher time per kernel.  This executor keeps the captured graph (its node
+// parameters: kernel arguments, grids, memcpy/memset descriptors) but issues it itself:
+//
+//   * nodes in a topological order that follows capture order (ties by creation index);
+//   * each node on one of at most `max_streams` HIP streams: a node continues the stream whose
+//     last node is one of its parents, else takes a stream whose last node is an ancestor (no
+//     false dependency), else opens a new stream, else (all streams busy with concurrent work)
+//     the stream whose tail was issued earliest;
+//   * a cross-stream edge becomes hipEventRecord / hipStreamWaitEvent, pruned with per-stream
+//     vector clocks (a wait is issued only when the consumer's stream does not already follow
+//     the producer's event transitively);
+//   * stream 0 is the caller's current stream; the others fork from it at the start of a replay
+//     and join into it at the end, so a replay is stream-ordered like hipGraphLaunch.
+//
+// Host cost per kernel is one hipLaunchKernel with the node's own argument block.  The graph
+// must outlive the executor (torch.cuda.CUDAGraph(keep_graph=True) keeps it).
+#include <ATen/hip/HIPContext.h>
+#include <c10/util/Exception.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <queue>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+#define GX_CHECK(expr)                                                                     \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    TORCH_CHECK(e_ == hipSuccess, "graphexec: ", #expr, " failed: ", hipGetErrorString(e_)); \
+  } while (0)
+
+enum NodeKind : int { kKernel = 0, kMemcpy, kMemset, kHost, kEmpty, kEvRecord, kEvWait };
+
+struct Node {
+  NodeKind kind = kEmpty;
+  hipKernelNodeParams kp{};
+  hipMemcpy3DParms cp{};
+  hipMemsetParams mp{};
+  hipHostNodeParams hp{};
+  hipEvent_t ext_event = nullptr;
+  int stream = 0;
+  std::vector<int> waits;  // indices (into `order`) of producer nodes whose event to wait on
+  int event = -1;          // index into events if a consumer on another stream waits on it
+};
+
+struct Exec {
+  std::vector<Node> nodes;  // issue order
+  std::vector<hipStream_t> streams;  // [0] is a placeholder: the caller's stream at replay
+  std::vector<hipEvent_t> events;
+  hipEvent_t fork = nullptr;
+  std::vector<hipEvent_t> joins;
+  int nstreams = 1;
+  int64_t counts[8] = {0};  // per NodeKind (kKernel..kEvWait) and the number of waits
+  ~Exec() {
+    for (auto e : events) (void)hipEventDestroy(e);
+    for (auto e : joins) (void)hipEventDestroy(e);
+    if (fork) (void)hipEventDestroy(fork);
+    for (size_t i = 1; i < streams.size(); ++i) (void)hipStreamDestroy(streams[i]);
+  }
+};
+
+Exec* as_exec(int64_t h) {
+  TORCH_CHECK(h != 0, "graphexec: null handle");
+  return reinterpret_cast<Exec*>(h);
+}
+
+int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
+  TORCH_CHECK(graph_handle != 0, "graphexec: null graph");
+  TORCH_CHECK(max_streams >= 1 && max_streams <= 8, "graphexec: 1..8 streams");
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph_handle);
+  size_t n = 0;
+  GX_CHECK(hipGraphGetNodes(g, nullptr, &n));
+  std::vector<hipGraphNode_t> raw(n);
+  if (n) GX_CHECK(hipGraphGetNodes(g, raw.data(), &n));
+  std::unordered_map<hipGraphNode_t, int> idx;
+  for (size_t i = 0; i < n; ++i) idx[raw[i]] = (int)i;
+  std::vector<std::vector<int>> parents(n), children(n);
+  for (size_t i = 0; i < n; ++i) {
+    size_t nd = 0;
+    GX_CHECK(hipGraphNodeGetDependencies(raw[i], nullptr, &nd));
+    std::vector<hipGraphNode_t> deps(nd);
+    if (nd) GX_CHECK(hipGraphNodeGetDependencies(raw[i], deps.data(), &nd));
+    for (auto d : deps) {
+      auto it = idx.find(d);
+      TORCH_CHECK(it != idx.end(), "graphexec: dependency outside the graph");
+      parents[i].push_back(it->second);
+      children[it->second].push_back((int)i);
+    }
+  }
+  // topological order, ties broken by creation index (= capture order)
+  std::vector<int> indeg(n), topo;
+  topo.reserve(n);
+  std::priority_queue<int, std::vector<int>, std::greater<int>> ready;
+  for (size_t i = 0; i < n; ++i) {
+    indeg[i] = (int)parents[i].size();
+    if (!indeg[i]) ready.push((int)i);
+  }
+  while (!ready.empty()) {
+    int v = ready.top();
+    ready.pop();
+    topo.push_back(v);
+    for (int c : children[v])
+      if (--indeg[c] == 0) ready.push(c);
+  }
+  TORCH_CHECK(topo.size() == n, "graphexec: graph has a cycle");
+  std::vector<int> pos(n);
+  for (size_t i = 0; i < n; ++i) pos[topo[i]] = (int)i;
+
+  auto ex = std::make_unique<Exec>();
+  ex->nodes.resize(n);
+  const int K = (int)max_streams;
+  // ancestor sets as bitsets over topo positions (n is a few thousand at most)
+  const size_t words = (n + 63) / 64;
+  std::vector<uint64_t> anc(n * words, 0);
+  auto is_anc = [&](int a_pos, int v_pos) {
+    return (anc[(size_t)v_pos * words + a_pos / 64] >> (a_pos % 64)) & 1ull;
+  };
+  std::vector<int> tail(K, -1);      // topo position of each stream's last node
+  std::vector<int> seq(n, 0);        // position of the node within its stream (1-based)
+  std::vector<int> slen(K, 0);
+  // vector clocks: clk[s][t] = last position on stream t that stream s already follows
+  std::vector<std::vector<int>> clk(K, std::vector<int>(K, 0));
+  std::vector<std::vector<int>> node_clk(n);
+  int used = 1;
+  for (size_t p = 0; p < n; ++p) {
+    int v = topo[p];
+    uint64_t* av = &anc[p * words];
+    for (int u : parents[v]) {
+      int up = pos[u];
+      const uint64_t* au = &anc[(size_t)up * words];
+      for (size_t w = 0; w < words; ++w) av[w] |= au[w];
+      av[up / 64] |= 1ull << (up % 64);
+    }
+    // stream choice
+    int s = -1;
+    for (int u : parents[v]) {  // continue a parent's stream (first parent in capture order)
+      for (int k = 0; k < used && s < 0; ++k)
+        if (tail[k] == pos[u]) s = k;
+      if (s >= 0) break;
+    }
+    if (s < 0)
+      for (int k = 0; k < used && s < 0; ++k)
+        if (tail[k] < 0 || is_anc(tail[k], (int)p)) s = k;
+    if (s < 0 && used < K) s = used++;
+    if (s < 0) {  // every stream runs concurrent work: the earliest tail serialises least
+      s = 0;
+      for (int k = 1; k < used; ++k)
+        if (tail[k] < tail[s]) s = k;
+    }
+    Node& nd = ex->nodes[p];
+    nd.stream = s;
+    // waits: parents on other streams that stream s does not already follow
+    for (int u : parents[v]) {
+      int up = pos[u];
+      int su = ex->nodes[up].stream;
+      if (su == s) continue;
+      if (clk[s][su] >= seq[up]) continue;
+      nd.waits.push_back(up);
+      const auto& uc = node_clk[up];
+      for (int k = 0; k < K; ++k) clk[s][k] = std::max(clk[s][k], uc[k]);
+    }
+    seq[p] = ++slen[s];
+    clk[s][s] = seq[p];
+    node_clk[p] = clk[s];
+    tail[s] = (int)p;
+  }
+  ex->nstreams = used;
+  // node parameters
+  for (size_t p = 0; p < n; ++p) {
+    Node& nd = ex->nodes[p];
+    hipGraphNode_t h = raw[topo[p]];
+    hipGraphNodeType t;
+    GX_CHECK(hipGraphNodeGetType(h, &t));
+    switch (t) {
+      case hipGraphNodeTypeKernel:
+        nd.kind = kKernel;
+        GX_CHECK(hipGraphKernelNodeGetParams(h, &nd.kp));
+        TORCH_CHECK(nd.kp.func != nullptr && (nd.kp.kernelParams != nullptr || nd.kp.extra == nullptr),
+                    "graphexec: kernel node with `extra` launch arguments is not supported");
+        break;
+      case hipGraphNodeTypeMemcpy:
+        nd.kind = kMemcpy;
+        GX_CHECK(hipGraphMemcpyNodeGetParams(h, &nd.cp));
+        break;
+      case hipGraphNodeTypeMemset:
+        nd.kind = kMemset;
+        GX_CHECK(hipGraphMemsetNodeGetParams(h, &nd.mp));
+        TORCH_CHECK(nd.mp.height <= 1 || nd.mp.elementSize == 1,
+                    "graphexec: 2-D memset of elements wider than a byte");
+        break;
+      case hipGraphNodeTypeHost:
+        nd.kind = kHost;
+        GX_CHECK(hipGraphHostNodeGetParams(h, &nd.hp));
+        break;
+      case hipGraphNodeTypeEmpty:
+        nd.kind = kEmpty;
+        break;
+      case hipGraphNodeTypeEventRecord:
+        nd.kind = kEvRecord;
+        GX_CHECK(hipGraphEventRecordNodeGetEvent(h, &nd.ext_event));
+        break;
+      case hipGraphNodeTypeWaitEvent:
+        nd.kind = kEvWait;
+        GX_CHECK(hipGraphEventWaitNodeGetEvent(h, &nd.ext_event));
+        break;
+      default:
+        TORCH_CHECK(false, "graphexec: unsupported graph node type ", (int)t);
+    }
+    ex->counts[nd.kind] += 1;
+    ex->counts[7] += (int64_t)nd.waits.size();
+  }
+  for (auto& nd : ex->nodes)
+    for (int w : nd.waits)
+      if (ex->nodes[w].event < 0) {
+        hipEvent_t e;
+        GX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ex->nodes[w].event = (int)ex->events.size();
+        ex->events.push_back(e);
+      }
+  ex->streams.assign(used, nullptr);
+  for (int k = 1; k < used; ++k) {
+    GX_CHECK(hipStreamCreateWithFlags(&ex->streams[k], hipStreamNonBlocking));
+    hipEvent_t e;
+    GX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ex->joins.push_back(e);
+  }
+  GX_CHECK(hipEventCreateWithFlags(&ex->fork, hipEventDisableTiming));
+  return reinterpret_cast<int64_t>(ex.release());
+}
+
+void issue(const Node& nd, hipStream_t st) {
+  switch (nd.kind) {
+    case kKernel:
+      GX_CHECK(hipLaunchKernel(nd.kp.func, nd.kp.gridDim, nd.kp.blockDim, nd.kp.kernelParams,
+                               nd.kp.sharedMemBytes, st));
+      break;
+    case kMemcpy:
+      GX_CHECK(hipMemcpy3DAsync(&nd.cp, st));
+      break;
+    case kMemset: {
+      const hipMemsetParams& m = nd.mp;
+      if (m.height > 1) {
+        GX_CHECK(hipMemset2DAsync(m.dst, m.pitch, (int)m.value, m.width, m.height, st));
+      } else if (m.elementSize == 1) {
+        GX_CHECK(hipMemsetD8Async(m.dst, (unsigned char)m.value, m.width, st));
+      } else if (m.elementSize == 2) {
+        GX_CHECK(hipMemsetD16Async(m.dst, (unsigned short)m.value, m.width, st));
+      } else {
+        GX_CHECK(hipMemsetD32Async(m.dst, (int)m.value, m.width, st));
+      }
+      break;
+    }
+    case kHost:
+      GX_CHECK(hipLaunchHostFunc(st, nd.hp.fn, nd.hp.userData));
+      break;
+    case kEvRecord:
+      GX_CHECK(hipEventRecord(nd.ext_event, st));
+      break;
+    case kEvWait:
+      GX_CHECK(hipStreamWaitEvent(st, nd.ext_event, 0));
+      break;
+    case kEmpty:
+      break;
+  }
+}
+
+void gexec_replay(int64_t h) {
+  Exec* ex = as_exec(h);
+  hipStream_t cur = at::hip::getCurrentHIPStream().stream();
+  ex->streams[0] = cur;
+  if (ex->nstreams > 1) {
+    GX_CHECK(hipEventRecord(ex->fork, cur));
+    for (int k = 1; k < ex->nstreams; ++k) GX_CHECK(hipStreamWaitEvent(ex->streams[k], ex->fork, 0));
+  }
+  for (const Node& nd : ex->nodes) {
+    hipStream_t st = ex->streams[nd.stream];
+    for (int w : nd.waits) GX_CHECK(hipStreamWaitEvent(st, ex->events[ex->nodes[w].event], 0));
+    issue(nd, st);
+    if (nd.event >= 0) GX_CHECK(hipEventRecord(ex->events[nd.event], st));
+  }
+  for (int k = 1; k < ex->nstreams; ++k) {
+    GX_CHECK(hipEventRecord(ex->joins[k - 1], ex->streams[k]));
+    GX_CHECK(hipStreamWaitEvent(cur, ex->joins[k - 1], 0));
+  }
+}
+
+// [kernels, memcpys, memsets, host, empty, event-record, event-wait, cross-stream waits,
+//  streams, recorded events]
+std::vector<int64_t> gexec_stats(int64_t h) {
+  Exec* ex = as_exec(h);
+  std::vector<int64_t> out(ex->counts, ex->counts + 8);
+  out.push_back(ex->nstreams);
+  out.push_back((int64_t)ex->events.size());
+  return out;
+}
+
+// per issued node: stream index (tests / tools: the schedule the heuristic produced)
+std::vector<int64_t> gexec_streams(int64_t h) {
+  Exec* ex = as_exec(h);
+  std::vector<int64_t> out;
+  out.reserve(ex->nodes.size());
+  for (const Node& nd : ex->nodes) out.push_back(nd.stream * 16 + (int64_t)nd.kind);
+  return out;
+}
+
+void gexec_destroy(int64_t h) {
+  if (h) delete as_exec(h);
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(simclr_amd, m) {
+  m.def("gexec_create(int graph, int max_streams) -> int", &gexec_create);
+  m.def("gexec_replay(int handle) -> ()", &gexec_replay);
+  m.def("gexec_stats(int handle) -> int[]", &gexec_stats);
+  m.def("gexec_streams(int handle) -> int[]", &gexec_streams);
+  m.def("gexec_destroy(int handle) -> ()", &gexec_destroy);
+}

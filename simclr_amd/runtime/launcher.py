@@ -81,11 +81,18 @@ def visible_gpu_count(kfd_nodes: str = KFD_NODES) -> Optional[int]:
     parent must never touch the GPU: ``torch.cuda.device_count()`` falls back to
     ``hipGetDeviceCount`` on ROCm when amdsmi is unavailable).  The visibility variables win
     when set; otherwise the KFD topology's GPU nodes (``simd_count > 0``; CPU nodes have 0) are
-    counted.  None when neither source is available."""
+    counted.  None when neither source is available.
+
+    The variables stack (ROCR filters the devices, HIP / CUDA filter what ROCR left), so the
+    count is the minimum over the ones that are set; a set but empty variable hides every GPU
+    (0, which callers treat as "no GPU visible", not "unknown")."""
+    counts = []
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
         if v is not None:
-            return len([t for t in v.split(",") if t.strip() != ""])
+            counts.append(len([t for t in v.split(",") if t.strip() != ""]))
+    if counts:
+        return min(counts)
     try:
         n = 0
         for node in sorted(os.listdir(kfd_nodes)):

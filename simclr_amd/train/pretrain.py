@@ -92,6 +92,10 @@ class Trainer:
             and self.precision == "bf16"
         self.model.train()
         self.graph = None
+        # how a captured step is issued: "graph" (hipGraphLaunch) or "streams" (the native
+        # multi-stream executor over the same captured nodes, runtime/graph_exec.py)
+        self.replay_mode = "graph"
+        self.sreplay = None
         self._static_x = None
         self._static_loss = None
         self.guard = StepGuard(st)
@@ -121,7 +125,10 @@ class Trainer:
         x = self.prepare(x)
         if self.graph is not None:
             self._static_x.copy_(x)
-            self.graph.replay()
+            if self.replay_mode == "streams" and self.sreplay is not None:
+                self.sreplay.replay()
+            else:
+                self.graph.replay()
             self.opt.host_step += 1
             loss = self._static_loss
         else:
@@ -129,8 +136,10 @@ class Trainer:
         self.guard.check(self.opt.host_step)
         return loss
 
-    def capture(self, x: torch.Tensor, warmup: int = 2) -> None:
-        """Capture one full training step into a hipGraph (after ``warmup`` eager steps)."""
+    def capture(self, x: torch.Tensor, warmup: int = 2, streams: int = 3) -> None:
+        """Capture one full training step into a hipGraph (after ``warmup`` eager steps) and
+        build the native multi-stream executor over its nodes (``streams`` > 0; kept as
+        ``self.sreplay``, selected by ``replay_mode = "streams"``)."""
         x = self.prepare(x)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -146,14 +155,23 @@ class Trainer:
             torch.cuda.synchronize(self.device)
             time.sleep(1.0)
         self._static_x = x.clone()
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         # with collectives in the step, the RCCL watchdog thread polls work events while the
         # capture is open: thread-local capture mode keeps those queries legal
         mode = "thread_local" if self.st.comm else "global"
         with torch.cuda.graph(g, capture_error_mode=mode):
             self._static_loss = self._step_body(self._static_x)
         self.opt.host_step -= 1  # the captured body incremented it once; replays add per step
+        g.instantiate()
         self.graph = g
+        self.sreplay = None
+        if streams > 0:
+            from ..runtime.graph_exec import StreamReplay
+            try:
+                self.sreplay = StreamReplay(g, max_streams=streams)
+            except RuntimeError as e:  # a node type the executor does not issue: graph only
+                log.warning("multi-stream replay unavailable: %s", e)
+                self.sreplay = None
 
 
 def pretrain(cfg) -> dict:

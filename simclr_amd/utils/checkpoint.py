@@ -133,6 +133,17 @@ def restore_rng(blob: dict, rank: Optional[int] = None) -> None:
     if ent.get("torch_rng") is not None:
         torch.set_rng_state(ent["torch_rng"])
     cuda = ent.get("cuda_rng_device")
+    if cuda is None and torch.cuda.is_available():
+        # resume files written before the per-rank entries: one device state per GPU, top level
+        legacy = blob.get("cuda_rng")
+        dev = torch.cuda.current_device()
+        if isinstance(legacy, (list, tuple)) and dev < len(legacy):
+            cuda = legacy[dev]
+        else:
+            import logging
+            logging.getLogger(__name__).warning(
+                "resume file holds no device RNG state for rank %d: the GPU augmentation stream "
+                "is NOT restored (it restarts from the seed)", rank)
     if cuda is not None and torch.cuda.is_available():
         torch.cuda.set_rng_state(cuda)
     n = ent.get("numpy_rng")

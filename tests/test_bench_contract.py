@@ -95,3 +95,16 @@ def test_visible_gpu_count_reads_kfd_topology(tmp_path, monkeypatch):
     assert visible_gpu_count(str(tmp_path / "missing")) is None
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert visible_gpu_count(str(tmp_path)) == 0
+
+
+def test_visible_gpu_count_stacks_variables(monkeypatch):
+    """ROCR filters the devices and HIP / CUDA filter what it left: the count is the minimum
+    over the variables that are set, and an empty one hides every GPU."""
+    from simclr_amd.runtime.launcher import visible_gpu_count
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert visible_gpu_count("/nonexistent") == 2
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "")
+    assert visible_gpu_count("/nonexistent") == 0

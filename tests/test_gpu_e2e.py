@@ -110,12 +110,23 @@ def test_hip_graph_replay_matches_eager():
 
 
 @pytest.mark.timeout(600)
-def test_golden_trajectory_resnet50_batch128_60_steps():
+@pytest.mark.parametrize("tuned", [False, True])
+def test_golden_trajectory_resnet50_batch128_60_steps(tuned, monkeypatch):
     """The flagship model trains on the bf16 HIP path: ResNet-50 (CIFAR stem), batch 128, 60
     optimizer steps (warmup + cosine, LARS) against the fp32 reference-semantics torch path
     from identical weights and views.  Both losses must fall by >= 0.3 (measured: 5.54 -> 4.8
-    on both paths) and the trajectories must agree (bounds below) — with the autotuner ON, i.e.
-    the tile variants production selects, not a pinned default set."""
+    on both paths) and the trajectories must agree:
+
+    * ``tuned=False``: the tiles pinned (autotuner off, fixed default variants, the
+      ``runtime.deterministic`` policy) and the tight bounds — a numerics change in a kernel
+      shows here without the tile choice moving underneath it;
+    * ``tuned=True``: the autotuner ON (the tiles production selects on this box, including the
+      weight-gradient variants 20-26) with looser running-mean bounds, since the chosen tiles'
+      summation orders vary from box to box."""
+    from simclr_amd.ops import tuning
+    monkeypatch.setattr(tuning, "ENABLED", tuning.ENABLED)  # both restored after the test
+    monkeypatch.setattr(tuning, "_CACHE", {})
+    tuning.set_enabled(tuned)
     from simclr_amd.data.datasets import synthetic_dataset
     from simclr_amd.data.loader import ContrastiveLoader
     from simclr_amd.config import compose, task_config, CONF_DIR
@@ -161,6 +172,13 @@ def test_golden_trajectory_resnet50_batch128_60_steps():
     first_h, last_h = sum(l_hip[:10]) / 10, sum(l_hip[-10:]) / 10
     first_r, last_r = sum(l_ref[:10]) / 10, sum(l_ref[-10:]) / 10
     assert last_h < first_h - 0.3 and last_r < first_r - 0.3, (first_h, last_h, first_r, last_r)
+    if not tuned:
+        # pinned tiles (the round-3 bounds): step-wise over 20 steps, 5-step running means
+        assert max(diffs[:20]) < 0.06, diffs[:20]
+        rm = [abs(sum(l_hip[i:i + 5]) - sum(l_ref[i:i + 5])) / 5 for i in range(len(xs) - 4)]
+        print("5-step running-mean |d| max", max(rm), "mean", sum(rm) / len(rm))
+        assert max(rm) < 0.12 and sum(rm) / len(rm) < 0.05, rm
+        return
     assert max(diffs[:5]) < 0.04, diffs[:5]
     rm = [abs(sum(l_hip[i:i + 10]) - sum(l_ref[i:i + 10])) / 10 for i in range(len(xs) - 9)]
     print("10-step running-mean |d| max", max(rm), "mean", sum(rm) / len(rm))

@@ -455,3 +455,50 @@ def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
             out = torch.empty(Co, k, k, C, device=DEV)
             ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, None, None, 0, False, 1, v)
             assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)
+
+
+@pytest.mark.parametrize("k,p,C,Co,H", [(3, 1, 128, 128, 16), (3, 1, 64, 128, 32),
+                                        (1, 0, 128, 256, 16), (3, 1, 256, 256, 8)])
+def test_igemm_dgrad_parity_classes_every_variant(ops, k, p, C, Co, H):
+    """Stride-2 input gradient as parity-class sub-convolutions (negative tap step, strided
+    output rows — the geometry models/fused.py ``_dgrad`` builds): every admissible tile variant,
+    register-staged and LDS-DMA, writes exactly its class's positions and matches fp32
+    ``conv2d_input`` there."""
+    from simclr_amd.models.fused import FusedStages, _ConvSpec
+    torch.manual_seed(17)
+    N, s = 8, 2
+    w = _bf(torch.randn(Co, C, k, k, device=DEV) / (C * k * k) ** 0.5)
+    OH = (H + 2 * p - k) // s + 1
+    dy = _bf(torch.randn(N, Co, OH, OH, device=DEV))
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float(), dy.float(), s, p).permute(0, 2, 3, 1)
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    wo = w.permute(0, 2, 3, 1).contiguous()
+    cs = _ConvSpec(torch.nn.Conv2d(C, Co, k, s, p, bias=False), None, s, k, p)
+    covered = torch.zeros(H, H, dtype=torch.bool, device=DEV)
+    seen_glds = False
+    for (r, c), prm in FusedStages._wt_params(cs):
+        wt = torch.empty((prm[3], prm[4], prm[5], prm[0]), device=DEV, dtype=torch.bfloat16)
+        ops.weight_transform(wo, wt, prm)
+        _, _, _, _, nkh, nkw, kh0, _, kw0, _ = prm
+        ohc, owc = (H - r + 1) // 2, (H - c + 1) // 2
+        g = [N, OH, OH, Co, ohc, owc, nkh, nkw, 1, 1, -1, -1, (r + p - kh0) // 2,
+             (c + p - kw0) // 2, C, H, H, 2, 2, r, c, C]
+        M = N * ohc * owc
+        n_ok = 0
+        for v in range(ops.igemm_nvariants()):
+            if not ops.igemm_variant_ok(v, g, False, False) or M % ops.igemm_variant_bm(v):
+                continue
+            dx = torch.full((N, H, H, C), float("nan"), device=DEV, dtype=torch.bfloat16)
+            ops.igemm(dyn, wt, dx, None, None, g, None, None, 0, False, 0, None, None, v,
+                      None, None, 0, 0, 0, None, None, None, None, None, None, None)
+            cls = dx[:, r::2, c::2]
+            assert _rel(cls, ref[:, r::2, c::2]) < 1e-2, (v, r, c)
+            mask = torch.ones(H, H, dtype=torch.bool, device=DEV)
+            mask[r::2, c::2] = False
+            assert bool(torch.isnan(dx[:, mask].float()).all()), ("wrote outside its class", v)
+            seen_glds |= ops.igemm_variant_glds(v)
+            n_ok += 1
+        assert n_ok >= 2, (r, c)
+        covered[r::2, c::2] = True
+    assert bool(covered.all()) or k == 1
+    assert seen_glds, "no LDS-DMA variant admitted the parity-class geometry"

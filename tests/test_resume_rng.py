@@ -74,3 +74,20 @@ def test_training_refuses_attribution_knobs(monkeypatch, knob):
     for fn in (pretrain, supervised):
         with pytest.raises(RuntimeError, match=knob):
             fn({})
+
+
+def test_restore_rng_legacy_device_state(monkeypatch, caplog):
+    """Resume files written before the per-rank entries keep the device generators as a
+    top-level ``cuda_rng`` list: the current device's entry is restored from it; a file with no
+    device state at all logs a warning instead of silently skipping the restore."""
+    from simclr_amd.utils import checkpoint as ck
+    seen = []
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 1)
+    monkeypatch.setattr(torch.cuda, "set_rng_state", lambda s: seen.append(s))
+    st = [torch.zeros(4, dtype=torch.uint8), torch.ones(4, dtype=torch.uint8)]
+    ck.restore_rng({"torch_rng": torch.get_rng_state(), "cuda_rng": st}, rank=0)
+    assert len(seen) == 1 and torch.equal(seen[0], st[1])
+    with caplog.at_level("WARNING"):
+        ck.restore_rng({"torch_rng": torch.get_rng_state()}, rank=0)
+    assert len(seen) == 1 and "NOT restored" in caplog.text
