@@ -259,8 +259,18 @@ def run_ours(args, rank, world, dev):
             host += time.perf_counter() - h0
         _sync(dev, world)
         t1 = time.perf_counter()
-        # host time spent issuing the steps (≈ wall time means the run is launch/CPU bound)
+        # host time spent issuing the steps (≈ wall time means the run is launch/CPU bound; with
+        # a replay the host also blocks whenever the device queue is full)
         args.host_issue_ms = host / args.steps * 1000.0
+        # the issue cost itself: steps issued onto an idle device (untimed, after the K steps)
+        idle = []
+        for _ in range(3):
+            _sync(dev, world)
+            h0 = time.perf_counter()
+            loss = tr.step(next_batch())
+            idle.append(time.perf_counter() - h0)
+        _sync(dev, world)
+        args.host_issue_idle_ms = min(idle) * 1000.0
         return t0, t1
 
     t0, t1 = measure()
@@ -438,6 +448,8 @@ def main(argv=None):
             "bn_comm_probe_ms_ipc_rccl": getattr(args, "comm_probe_ms", None),
             "host_issue_ms_per_step": (round(args.host_issue_ms, 3)
                                        if hasattr(args, "host_issue_ms") else None),
+            "host_issue_ms_idle_device": (round(args.host_issue_idle_ms, 3)
+                                          if hasattr(args, "host_issue_idle_ms") else None),
             "final_loss": loss,
         },
     }

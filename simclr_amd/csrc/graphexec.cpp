@@ -191,10 +191,19 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
       case hipGraphNodeTypeMemcpy:
         nd.kind = kMemcpy;
         GX_CHECK(hipGraphMemcpyNodeGetParams(h, &nd.cp));
+        // a node captured from a 1-D hipMemcpyAsync reports no 3-D descriptor (HIP keeps its
+        // 1-D parameters privately): refuse at build time, the caller keeps hipGraphLaunch
+        TORCH_CHECK((nd.cp.srcPtr.ptr != nullptr || nd.cp.srcArray != nullptr) &&
+                        (nd.cp.dstPtr.ptr != nullptr || nd.cp.dstArray != nullptr) &&
+                        nd.cp.extent.width > 0,
+                    "graphexec: memcpy node without a readable 3-D descriptor (1-D capture)");
         break;
       case hipGraphNodeTypeMemset:
         nd.kind = kMemset;
         GX_CHECK(hipGraphMemsetNodeGetParams(h, &nd.mp));
+        TORCH_CHECK(nd.mp.dst != nullptr && nd.mp.width > 0 &&
+                        (nd.mp.elementSize == 1 || nd.mp.elementSize == 2 || nd.mp.elementSize == 4),
+                    "graphexec: memset node without readable parameters");
         TORCH_CHECK(nd.mp.height <= 1 || nd.mp.elementSize == 1,
                     "graphexec: 2-D memset of elements wider than a byte");
         break;

@@ -29,8 +29,7 @@ def test_stream_replay_two_stream_dag():
         c.mul_(c)
         torch.cuda.current_stream(dev).wait_stream(side)
         out = c - b
-        snap = torch.empty_like(out)
-        snap.copy_(out)
+        snap = out * 1.0
         zeros = torch.zeros(4096, device=dev)
     g.instantiate()
     r = StreamReplay(g, max_streams=3)
@@ -51,6 +50,31 @@ def test_stream_replay_two_stream_dag():
         r.replay()
     torch.cuda.synchronize()
     r.close()
+
+
+def test_stream_replay_refuses_unreadable_memcpy_nodes():
+    """A D2D copy captured from hipMemcpyAsync is a 1-D memcpy node whose parameters HIP does
+    not expose: the executor must refuse it when it is BUILT (the trainer then keeps
+    hipGraphLaunch), never fail at replay time."""
+    from simclr_amd.runtime.graph_exec import StreamReplay
+    dev = torch.device("cuda", 0)
+    a = torch.randn(1 << 16, device=dev)
+    b = torch.empty_like(a)
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g):
+        b.copy_(a)
+        c = b * 2
+    g.instantiate()
+    try:
+        r = StreamReplay(g, max_streams=2)
+    except RuntimeError as e:
+        assert "memcpy" in str(e)
+        return
+    # the runtime exposed a readable descriptor: then the replay must be right
+    a.normal_()
+    r.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(c, a * 2)
 
 
 def _trainer(base, stem, batch):
