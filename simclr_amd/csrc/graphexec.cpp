@@ -5,7 +5,7 @@
 // the eager schedule (the weight gradients on their side stream no longer overlap the
 // dgrad/BatchNorm chain: profiles/r4_optimization_log.md), while eager issue costs ~30 µs of
 // Python + dispatcher time per kernel.  This executor keeps the captured graph (its node
-// parameters: kernel arguments, grids, memcpy/memset descriptors) but issues it itself:
+// parameters: kernel arguments, grids, memset descriptors) but issues it itself:
 //
 //   * nodes in a topological order that follows capture order (ties by creation index);
 //   * each node on one of at most `max_streams` HIP streams: a node continues the stream whose
@@ -39,12 +39,15 @@ namespace {
     TORCH_CHECK(e_ == hipSuccess, "graphexec: ", #expr, " failed: ", hipGetErrorString(e_)); \
   } while (0)
 
-enum NodeKind : int { kKernel = 0, kMemcpy, kMemset, kHost, kEmpty, kEvRecord, kEvWait };
+// kSub: any other node (memcpy nodes — HIP does not expose the parameters of one captured from a
+// 1-D hipMemcpyAsync —, child graphs, ...) replayed as a one-node executable graph cut from a
+// clone of the captured graph
+enum NodeKind : int { kKernel = 0, kSub, kMemset, kHost, kEmpty, kEvRecord, kEvWait };
 
 struct Node {
   NodeKind kind = kEmpty;
   hipKernelNodeParams kp{};
-  hipMemcpy3DParms cp{};
+  hipGraphExec_t sub = nullptr;
   hipMemsetParams mp{};
   hipHostNodeParams hp{};
   hipEvent_t ext_event = nullptr;
@@ -62,6 +65,8 @@ struct Exec {
   int nstreams = 1;
   int64_t counts[8] = {0};  // per NodeKind (kKernel..kEvWait) and the number of waits
   ~Exec() {
+    for (auto& nd : nodes)
+      if (nd.sub) (void)hipGraphExecDestroy(nd.sub);
     for (auto e : events) (void)hipEventDestroy(e);
     for (auto e : joins) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
@@ -72,6 +77,24 @@ struct Exec {
 Exec* as_exec(int64_t h) {
   TORCH_CHECK(h != 0, "graphexec: null handle");
   return reinterpret_cast<Exec*>(h);
+}
+
+// a one-node executable graph performing `node` of `g` (cloned, every other node removed)
+hipGraphExec_t single_node_exec(hipGraph_t g, hipGraphNode_t node) {
+  hipGraph_t c;
+  GX_CHECK(hipGraphClone(&c, g));
+  hipGraphNode_t keep;
+  GX_CHECK(hipGraphNodeFindInClone(&keep, node, c));
+  size_t n = 0;
+  GX_CHECK(hipGraphGetNodes(c, nullptr, &n));
+  std::vector<hipGraphNode_t> all(n);
+  if (n) GX_CHECK(hipGraphGetNodes(c, all.data(), &n));
+  for (auto x : all)
+    if (x != keep) GX_CHECK(hipGraphDestroyNode(x));
+  hipGraphExec_t e;
+  GX_CHECK(hipGraphInstantiate(&e, c, nullptr, nullptr, 0));
+  GX_CHECK(hipGraphDestroy(c));
+  return e;
 }
 
 int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
@@ -188,16 +211,6 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
         TORCH_CHECK(nd.kp.func != nullptr && (nd.kp.kernelParams != nullptr || nd.kp.extra == nullptr),
                     "graphexec: kernel node with `extra` launch arguments is not supported");
         break;
-      case hipGraphNodeTypeMemcpy:
-        nd.kind = kMemcpy;
-        GX_CHECK(hipGraphMemcpyNodeGetParams(h, &nd.cp));
-        // a node captured from a 1-D hipMemcpyAsync reports no 3-D descriptor (HIP keeps its
-        // 1-D parameters privately): refuse at build time, the caller keeps hipGraphLaunch
-        TORCH_CHECK((nd.cp.srcPtr.ptr != nullptr || nd.cp.srcArray != nullptr) &&
-                        (nd.cp.dstPtr.ptr != nullptr || nd.cp.dstArray != nullptr) &&
-                        nd.cp.extent.width > 0,
-                    "graphexec: memcpy node without a readable 3-D descriptor (1-D capture)");
-        break;
       case hipGraphNodeTypeMemset:
         nd.kind = kMemset;
         GX_CHECK(hipGraphMemsetNodeGetParams(h, &nd.mp));
@@ -222,8 +235,10 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
         nd.kind = kEvWait;
         GX_CHECK(hipGraphEventWaitNodeGetEvent(h, &nd.ext_event));
         break;
-      default:
-        TORCH_CHECK(false, "graphexec: unsupported graph node type ", (int)t);
+      default:  // memcpy, child graph, ...: a one-node graph of its own
+        nd.kind = kSub;
+        nd.sub = single_node_exec(g, h);
+        break;
     }
     ex->counts[nd.kind] += 1;
     ex->counts[7] += (int64_t)nd.waits.size();
@@ -253,8 +268,8 @@ void issue(const Node& nd, hipStream_t st) {
       GX_CHECK(hipLaunchKernel(nd.kp.func, nd.kp.gridDim, nd.kp.blockDim, nd.kp.kernelParams,
                                nd.kp.sharedMemBytes, st));
       break;
-    case kMemcpy:
-      GX_CHECK(hipMemcpy3DAsync(&nd.cp, st));
+    case kSub:
+      GX_CHECK(hipGraphLaunch(nd.sub, st));
       break;
     case kMemset: {
       const hipMemsetParams& m = nd.mp;
@@ -303,8 +318,8 @@ void gexec_replay(int64_t h) {
   }
 }
 
-// [kernels, memcpys, memsets, host, empty, event-record, event-wait, cross-stream waits,
-//  streams, recorded events]
+// [kernels, one-node sub-graphs, memsets, host, empty, event-record, event-wait, cross-stream
+//  waits, streams, recorded events]
 std::vector<int64_t> gexec_stats(int64_t h) {
   Exec* ex = as_exec(h);
   std::vector<int64_t> out(ex->counts, ex->counts + 8);

@@ -1,0 +1,213 @@
+"""Fused projection head: ``Linear(H,H)+b → BN1d → ReLU → Linear(H,d)`` as one
+short launch sequence on the MFMA implicit-GEMM kernels, instead of a chain of per-op autograd
+nodes (tests/test_gpu_head.py counts both).
+
+Reference: ``ProjectionHead`` (``/root/reference/model.py:56-73``) with its BatchNorm1d converted
+to SyncBatchNorm (main.py:176) and the two views run as separate forwards (main.py:112-113, so
+the statistics are per view: SURVEY Q17).  Same math; what changes is where the BatchNorm work
+runs (S = 2 view segments, statistics per segment, all-reduced across ranks)::
+
+    forward   y1 = x·W1ᵀ + b1            GEMM 1, epilogue: bias + Σ, Σ² partials of y1
+              finalize                   one launch: mean / invstd, running stats, scale/shift
+                                         (the cross-GPU statistics combine happens here)
+              z = relu(bn(y1))·W2ᵀ       GEMM 2, the BN + ReLU applied to its A operand in the
+                                         prologue: relu(bn(y1)) is never written to HBM
+              (+ the transposed weights W1ᵀ, W2ᵀ for the backward: one batched launch)
+    backward  g = (dz·W2)·[bn(y1) > 0]   dgrad 2, epilogue: ReLU mask + Σg, Σg·x̂ partials
+              dW2 = dzᵀ·relu(bn(y1))     weight gradient, the BN + ReLU in the X prologue
+              finalize                   dγ, dβ (flat gradient buffer) and the input-gradient
+                                         coefficients; cross-GPU combine here
+              dx = (A·g + B·y1 + D)·W1   dgrad 1, the BN backward in the A-operand prologue:
+                                         the BN's input gradient is never written to HBM
+              dW1 = (A·g + B·y1 + D)ᵀ·x  weight gradient, the same prologue on its dY operand
+
+The gradient of b1 is exactly zero: a bias in front of a BatchNorm cancels in (y − mean(y)),
+so dL/db1 = Σ_rows dL/dy1 = 0 for every view over the global batch (the reference's autograd
+produces that zero up to fp32 round-off; the data-parallel average of per-rank values is the
+same zero).  Its slot in the flat gradient buffer is zeroed once and left alone.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..ops import _ext
+from ..ops.conv_hip import igemm_choose, igemm_launch, run_wgrad
+from ..parallel import state as pstate
+
+
+def _geom(M, K, N):
+    return [M, 1, 1, K, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, N, 1, 1, 1, 1, 0, 0, N]
+
+
+def _w16(weight: torch.Tensor) -> torch.Tensor:
+    slot = getattr(weight, "_slot", None)
+    if slot is not None and slot.shadow is not None:
+        return slot.shadow
+    return weight.detach().to(torch.bfloat16).contiguous()
+
+
+def _bnops():
+    from .fused import FusedStages
+    return FusedStages.__new__(FusedStages)  # the stateless BatchNorm helpers of the executor
+
+
+def _deliver(param: torch.Tensor, compute) -> Optional[torch.Tensor]:
+    """``compute(out)`` writes the fp32 gradient of ``param`` into its flat-store slot (and
+    notifies the reducer); returns the gradient tensor for autograd when unbound."""
+    slot = getattr(param, "_slot", None)
+    if slot is not None:
+        compute(slot.grad)
+        slot.store.mark_ready(slot.index)
+        return None
+    g = torch.empty(param.shape, device=param.device, dtype=torch.float32)
+    compute(g)
+    return g
+
+
+def eligible(mod, x: torch.Tensor, segments: int) -> bool:
+    """bf16 GPU rows, per-view row counts that tile evenly (256-row BN-backward prologue tiles),
+    and feature sizes the LDS-DMA tiles take (multiples of 64)."""
+    s = mod._seq
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and mod.training):
+        return False
+    if not getattr(s.bn1, "training", True):
+        return False
+    M, K = x.shape
+    H, D = s.linear1.out_features, s.linear2.out_features
+    return (M % segments == 0 and (M // segments) % 256 == 0 and K % 64 == 0 and H % 64 == 0
+            and D % 64 == 0 and s.linear1.bias is not None and s.linear2.in_features == H)
+
+
+class MLPHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, gamma, beta, w2, b2, mod, S):
+        ops = _ext.ops()
+        st = pstate.get()
+        s = mod._seq
+        lin1, bn, lin2 = s.linear1, s.bn1, s.linear2
+        M, K = x.shape
+        H, D = lin1.out_features, lin2.out_features
+        seg = M // S
+        dev = x.device
+        xc = x.contiguous()
+        W1, W2 = _w16(lin1.weight), _w16(lin2.weight)
+        # GEMM 1: bias + BatchNorm statistics partials
+        y1 = torch.empty((M, H), device=dev, dtype=torch.bfloat16)
+        g1 = _geom(M, K, H)
+        bias1 = b1.detach().float().contiguous()
+        v = igemm_choose(ops, xc, W1, y1, g1, bias=bias1, want_stats=True, seg_rows=seg)
+        bm = ops.igemm_variant_bm(v)
+        part = torch.empty(((M // bm) * 2 * H,), device=dev, dtype=torch.float32)
+        igemm_launch(ops, xc, W1, y1, g1, v, bias=bias1, stats=part)
+        bs = _bnops()._bn_fwd(ops, bn, part, seg // bm, seg, S, st)
+        # GEMM 2 on relu(bn(y1)) formed in the operand prologue
+        z = torch.empty((M, D), device=dev, dtype=torch.bfloat16)
+        g2 = _geom(M, H, D)
+        pro = (bs.ss[0], bs.ss[1], seg, True)
+        bias2 = b2.detach().float().contiguous() if b2 is not None else None
+        v2 = igemm_choose(ops, y1, W2, z, g2, bias=bias2, pro=pro, seg_rows=seg)
+        igemm_launch(ops, y1, W2, z, g2, v2, bias=bias2, pro=pro)
+        # the backward's transposed weights, one batched launch (weights are final until the
+        # optimizer step, which comes after the backward)
+        wt1, wt2 = _transposed(ops, mod, W1, W2, K, H, D)
+        ctx.save_for_backward(xc, y1)
+        ctx.bs = bs
+        ctx.mod = mod
+        ctx.wts = (wt1, wt2)
+        ctx.S = S
+        ctx.has_b2 = b2 is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        ops = _ext.ops()
+        st = pstate.get()
+        xc, y1 = ctx.saved_tensors
+        bs, mod, S = ctx.bs, ctx.mod, ctx.S
+        wt1, wt2 = ctx.wts
+        s = mod._seq
+        lin1, bn, lin2 = s.linear1, s.bn1, s.linear2
+        M, K = xc.shape
+        H, D = lin1.out_features, lin2.out_features
+        seg = M // S
+        dev = dz.device
+        dzc = dz.contiguous()
+        if dzc.dtype != torch.bfloat16:
+            dzc = dzc.to(torch.bfloat16)
+        bnx = _bnops()
+        # dgrad 2: g = (dz·W2)·[bn(y1) > 0] with the BN-backward partials Σg, Σg·x̂
+        gm = torch.empty((M, H), device=dev, dtype=torch.bfloat16)
+        gd = _geom(M, D, H)
+        epi = (3, None, y1)
+        tables = (bs.ss.view(-1), bs.mi)
+        v = igemm_choose(ops, dzc, wt2, gm, gd, want_stats=True, epi=epi, seg_rows=seg,
+                         epi_tables=tables)
+        nb = seg // ops.igemm_variant_bm(v)
+        part = torch.empty((S * nb * 2 * H,), device=dev, dtype=torch.float32)
+        igemm_launch(ops, dzc, wt2, gm, gd, v, stats=part, epi=epi, seg_rows=seg,
+                     epi_tables=tables, remap=(nb, 0))
+        h = bnx._bn_bwd_start(ops, bn, part, nb, bs, S, st)
+        # dW2 = dzᵀ · relu(bn(y1)) (X prologue), independent of the BN backward
+        pro = (bs.ss[0], bs.ss[1], seg, True, S)
+        gw2 = _deliver(lin2.weight, lambda o: run_wgrad(ops, dzc, y1, o.view(D, 1, 1, H),
+                                                        _geom(M, H, D), H, pro=pro))
+        gb2 = None
+        if ctx.has_b2:
+            gb2 = _deliver(lin2.bias, lambda o: ops.colsum(dzc, o, 0.0))
+        coef = bnx._bn_bwd_finish(ops, h, S)
+        # dgrad 1 with the BN backward da = A·g + B·y1 + D in the A-operand prologue
+        SC = S * H
+        bpro = (coef[:SC], coef[SC:2 * SC], coef[2 * SC:], seg, y1)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, K), device=dev, dtype=torch.bfloat16)
+            gx = _geom(M, H, K)
+            v = igemm_choose(ops, gm, wt1, dx, gx, bnb=bpro)
+            igemm_launch(ops, gm, wt1, dx, gx, v, bnb=bpro)
+        # dW1 = daᵀ · x, the same prologue on the dY operand
+        gw1 = _deliver(lin1.weight, lambda o: run_wgrad(ops, gm, xc, o.view(H, 1, 1, K),
+                                                        _geom(M, K, H), K,
+                                                        dpro=(y1, coef, seg, S)))
+        gb1 = _zero_bias_grad(lin1.bias)
+        return dx, gw1, gb1, None, None, gw2, gb2, None, None
+
+
+def _zero_bias_grad(bias: torch.Tensor) -> Optional[torch.Tensor]:
+    slot = getattr(bias, "_slot", None)
+    if slot is None:
+        return torch.zeros(bias.shape, device=bias.device, dtype=torch.float32)
+    if not getattr(slot, "_static_zero", False):
+        slot.grad.zero_()  # once: nothing else ever writes this slot
+        slot._static_zero = True
+    slot.store.mark_ready(slot.index)
+    return None
+
+
+def _transposed(ops, mod, W1, W2, K, H, D):
+    """W1ᵀ [K][H] and W2ᵀ [H][D] (the dgrads' B operands) in one batched launch; the plan is
+    rebuilt when the bf16 weights move (never during a graph capture: the first eager step
+    builds it)."""
+    sig = (W1.data_ptr(), W2.data_ptr(), K, H, D)
+    cache = mod.__dict__.get("_head_wt")
+    if cache is None or cache[0] != sig:
+        dev = W1.device
+        wt1 = torch.empty((K, 1, 1, H), device=dev, dtype=torch.bfloat16)
+        wt2 = torch.empty((H, 1, 1, D), device=dev, dtype=torch.bfloat16)
+        params = [H, 1, 1, K, 1, 1, 0, 1, 0, 1, D, 1, 1, H, 1, 1, 0, 1, 0, 1]
+        plan = ops.weight_transform_plan([W1, W2], [wt1, wt2], params)
+        cache = (sig, plan[:-1].to(dev), int(plan[-1]), wt1, wt2, (W1, W2))
+        mod.__dict__["_head_wt"] = cache
+    ops.weight_transform_batch(cache[1], cache[2])
+    return cache[3].view(K, H), cache[4].view(H, D)
+
+
+def fused_mlp(mod, x: torch.Tensor, segments: int) -> Optional[torch.Tensor]:
+    """The fused head's output, or None when the shapes / mode are not eligible."""
+    if not eligible(mod, x, segments):
+        return None
+    _ext.require()
+    s = mod._seq
+    return MLPHeadFn.apply(x, s.linear1.weight, s.linear1.bias, s.bn1.weight, s.bn1.bias,
+                           s.linear2.weight, s.linear2.bias, mod, segments)

@@ -52,8 +52,16 @@ class _MLP(nn.Module):
     def _seq(self) -> nn.Sequential:
         return getattr(self, self._attr)
 
+    # the fused GEMM-BN-GEMM schedule (models/head_fused.py) for eligible training batches
+    use_fused = True
+
     def forward(self, x: torch.Tensor, segments: int = 1) -> torch.Tensor:
         s = self._seq
+        if self.training and self.use_fused and x.is_cuda:
+            from .head_fused import fused_mlp
+            out = fused_mlp(self, x, segments)
+            if out is not None:
+                return out
         h = s.linear1(x)
         h = s.bn1(h, relu=True, segments=segments)
         return s.linear2(h)

@@ -17,7 +17,7 @@ import torch
 
 from ..ops import _ext
 
-STAT_NAMES = ("kernels", "memcpys", "memsets", "host", "empty", "event_records", "event_waits",
+STAT_NAMES = ("kernels", "subgraphs", "memsets", "host", "empty", "event_records", "event_waits",
               "cross_stream_waits", "streams", "events")
 
 

@@ -8,7 +8,14 @@ percent.  A comparison at that noise floor cannot see a few-percent kernel defec
 
   * every residual block's last BatchNorm starts at γ = ``gamma_last`` (the "zero-init residual"
     recipe with a non-zero value, so every weight still gets a gradient): each block is close to
-    the identity, rounding errors no longer amplify from stage to stage;
+    the identity, rounding errors no longer amplify from stage to stage (measured: 0.6 % at
+    layer1 → 2.6 % at layer4 on both bf16 paths);
+  * every other BatchNorm starts at γ = 0.25, β = 1, so a ReLU input sits ~4 σ above zero: at
+    init the ReLU masks are what makes the gradient chaotic — a 1-2 % rounding difference flips
+    the masks of the units near zero, and a flipped unit passes its whole gradient or none, so
+    with the default init BOTH bf16 paths' parameter gradients were 30 % (ResNet-50) / 15 %
+    (ResNet-18) from fp32 for EVERY parameter (measured) even though the forward agreed to 2 %.
+    The mask logic itself (mode 3 / 4 epilogues, block-output bitmask) has per-kernel tests;
   * the backward is driven by a fixed random projection of the backbone features h (the fused
     executor's output after the average pool), L = Σ h·R / N, instead of NT-Xent on the
     projection head's z: at init the features of different images are nearly equal, so the
@@ -32,9 +39,10 @@ def _bf(t):
     return t.to(torch.bfloat16)
 
 
-def _model(base, stem, device, gamma_last):
+def _model(base, stem, device, gamma_last, gamma=0.25, beta=1.0):
     from simclr_amd.models.contrastive import ContrastiveModel
     from simclr_amd.models.resnet import BasicBlock, Bottleneck
+    from simclr_amd.ops.batchnorm import _BatchNormBase
     from simclr_amd.parallel import state as pstate
     from simclr_amd.parallel.flat import FlatParamStore
     pstate.reset()
@@ -43,6 +51,10 @@ def _model(base, stem, device, gamma_last):
     m = ContrastiveModel(base_cnn=base, d=128, cifar_stem=stem).to(device)
     if gamma_last is not None:
         with torch.no_grad():
+            for mod in m.f.modules():
+                if isinstance(mod, _BatchNormBase):
+                    mod.weight.fill_(gamma)
+                    mod.bias.fill_(beta)
             for mod in m.f.modules():
                 if isinstance(mod, Bottleneck):
                     mod.bn3.weight.fill_(gamma_last)
@@ -75,6 +87,15 @@ def run_three(base, stem, batch, monkeypatch, block_out=True, gamma_last=0.2, mu
             stages["fused"][b.name.split(".")[0]] = tp.out.float().permute(0, 3, 1, 2).clone()
         return out, tapes
     monkeypatch.setattr(FusedStages, "forward", rec_fwd)
+    bstages = {}  # mode -> {stage: gradient w.r.t. the stage's input (fp32, NCHW)}
+    orig_bb = FusedStages._block_backward
+
+    def rec_bb(self, ops, st, S, b, tp, g, pre, prev):
+        dx, h = orig_bb(self, ops, st, S, b, tp, g, pre, prev)
+        if b.name.endswith(".0"):  # the input of a stage's first block
+            bstages["fused"][b.name.split(".")[0]] = dx.float().permute(0, 3, 1, 2).clone()
+        return dx, h
+    monkeypatch.setattr(FusedStages, "_block_backward", rec_bb)
     if mutate is not None:
         kind, bname, ci = mutate
         if kind == "fwd":
@@ -104,12 +125,19 @@ def run_three(base, stem, batch, monkeypatch, block_out=True, gamma_last=0.2, mu
         m2, store2 = _model(base, stem, dev, gamma_last)
         m2.f.use_fused_stages = mode == "fused"
         stages[mode] = {}
+        bstages[mode] = {}
         hooks = []
         if mode != "fused":
             for ln in STAGES:
                 hooks.append(getattr(m2.f, ln)[-1].register_forward_hook(
                     lambda mod, inp, out, ln=ln, mode=mode:
                     stages[mode].__setitem__(ln, out.detach().float().clone())))
+
+                def pre(mod, inp, ln=ln, mode=mode):
+                    if inp[0].requires_grad:
+                        inp[0].register_hook(lambda g, ln=ln, mode=mode: bstages[mode].__setitem__(
+                            ln, g.detach().float().clone()))
+                hooks.append(getattr(m2.f, ln)[0].register_forward_pre_hook(pre))
         if mode == "fp32":
             with torch.no_grad():  # same (bf16-representable) weights, fp32 compute
                 store2.master.copy_(store2.shadow.float())
@@ -118,7 +146,7 @@ def run_three(base, stem, batch, monkeypatch, block_out=True, gamma_last=0.2, mu
                 sl.shadow = None
         store2.zero_grad()
         xin = x.float()[:, :3].contiguous() if mode == "fp32" else x
-        if loss == "projection":  # the backbone alone (the fused executor's output) drives it
+        if loss in ("projection", "energy"):  # the backbone alone (the executor's output)
             z = m2.encode(xin, segments=2)
         else:
             z = m2(xin, segments=2)
@@ -126,6 +154,8 @@ def run_three(base, stem, batch, monkeypatch, block_out=True, gamma_last=0.2, mu
             proj = torch.randn(z.shape, device=dev, dtype=torch.float32)
         if loss == "projection":
             lval = (z.float() * proj).sum() / z.shape[0]
+        elif loss == "energy":
+            lval = 0.5 * (z.float() * (z.float() + proj)).sum() / z.shape[0]
         else:
             lval = NTXent(temperature=0.5)(z)
         lval.backward()
@@ -146,14 +176,21 @@ def run_three(base, stem, batch, monkeypatch, block_out=True, gamma_last=0.2, mu
 
     out = {"stage": {}, "param": {}, "buffers": {}, "launch_counts": res["launch_counts"],
            "loss": (res["fused"][0], res["module"][0], res["fp32"][0])}
+    out["stage_fm"], out["param_fm"], out["bstage"] = {}, {}, {}
+    for ln in STAGES:
+        w = bstages["fp32"].get(ln)
+        if w is not None and ln in bstages["fused"] and ln in bstages["module"]:
+            out["bstage"][ln] = (rel(bstages["fused"][ln], w), rel(bstages["module"][ln], w))
     for ln in STAGES:
         w = stages["fp32"][ln]
         out["stage"][ln] = (rel(stages["fused"][ln], w), rel(stages["module"][ln], w))
+        out["stage_fm"][ln] = rel(stages["fused"][ln], stages["module"][ln])
     for (o, n_), name in zip(store.segments(), store.names):
         w = gr[o:o + n_]
         if w.norm().item() < 1e-8:
             continue
         out["param"][name] = (rel(gf[o:o + n_], w), rel(gm[o:o + n_], w))
+        out["param_fm"][name] = rel(gf[o:o + n_], gm[o:o + n_])
     out["total_grad"] = (rel(gf, gr), rel(gm, gr))
     for (name, u), (_, v), (_, w) in zip(res["fused"][2], res["module"][2], res["fp32"][2]):
         out["buffers"][name] = (rel(u, w), rel(v, w))
@@ -199,7 +236,13 @@ def summary(mt, top=6):
                    key=lambda t: -t[1])[:top]
     convs = [kv for kv in mt["param"].items() if "conv" in kv[0] or "downsample.0" in kv[0]]
     bns = [kv for kv in mt["param"].items() if kv not in convs]
+    fm = sorted(mt["param_fm"].items(), key=lambda kv: -kv[1])
+    fmc = [v for k, v in fm if "conv" in k or "downsample.0" in k]
     return {"stage": {k: (round(a, 5), round(b, 5)) for k, (a, b) in mt["stage"].items()},
+            "stage_fm": {k: round(v, 5) for k, v in mt["stage_fm"].items()},
+            "bstage": {k: (round(a, 5), round(b, 5)) for k, (a, b) in mt["bstage"].items()},
+            "fm_conv_q50_q90_max": _dist(fmc),
+            "fm_worst": [(k, round(v, 5)) for k, v in fm[:top]],
             "conv_grad_q50_q90_max": (_dist([a for _, (a, b) in convs]),
                                       _dist([b for _, (a, b) in convs])),
             "bn_grad_q50_q90_max": (_dist([a for _, (a, b) in bns]),

@@ -52,29 +52,28 @@ def test_stream_replay_two_stream_dag():
     r.close()
 
 
-def test_stream_replay_refuses_unreadable_memcpy_nodes():
+def test_stream_replay_memcpy_nodes_as_subgraphs():
     """A D2D copy captured from hipMemcpyAsync is a 1-D memcpy node whose parameters HIP does
-    not expose: the executor must refuse it when it is BUILT (the trainer then keeps
-    hipGraphLaunch), never fail at replay time."""
+    not expose: the executor replays it as a one-node graph cut from a clone, in order with the
+    kernels around it on its stream."""
     from simclr_amd.runtime.graph_exec import StreamReplay
     dev = torch.device("cuda", 0)
     a = torch.randn(1 << 16, device=dev)
     b = torch.empty_like(a)
     g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g):
-        b.copy_(a)
+        a2 = a + 1
+        b.copy_(a2)
         c = b * 2
     g.instantiate()
-    try:
-        r = StreamReplay(g, max_streams=2)
-    except RuntimeError as e:
-        assert "memcpy" in str(e)
-        return
-    # the runtime exposed a readable descriptor: then the replay must be right
-    a.normal_()
-    r.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(c, a * 2)
+    r = StreamReplay(g, max_streams=2)
+    st = r.stats()
+    assert st["subgraphs"] >= 1 and st["kernels"] >= 2, st
+    for _ in range(3):
+        a.normal_()
+        r.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(b, a + 1) and torch.equal(c, (a + 1) * 2)
 
 
 def _trainer(base, stem, batch):
@@ -118,7 +117,8 @@ def test_stream_replay_matches_graph_replay(base, stem, batch):
     c.replay_mode = "streams"
     stats = c.sreplay.stats()
     print("stream replay", stats)
-    assert stats["kernels"] > 100 and stats["streams"] >= 2, stats
+    # (ResNet-18 at batch 32 runs the per-module path: one stream)
+    assert stats["kernels"] > 100 and stats["streams"] >= (2 if base == "resnet50" else 1), stats
     lb = [float(b.step(x).item()) for x in xs[1:]]
     lc = [float(c.step(x).item()) for x in xs[1:]]
     torch.cuda.synchronize()
