@@ -170,17 +170,19 @@ class MLPHeadFn(torch.autograd.Function):
         gw1 = _deliver(lin1.weight, lambda o: run_wgrad(ops, gm, xc, o.view(H, 1, 1, K),
                                                         _geom(M, K, H), K,
                                                         dpro=(y1, coef, seg, S)))
-        gb1 = _zero_bias_grad(lin1.bias)
+        gb1 = _zero_bias_grad(mod, lin1.bias)
         return dx, gw1, gb1, None, None, gw2, gb2, None, None
 
 
-def _zero_bias_grad(bias: torch.Tensor) -> Optional[torch.Tensor]:
+def _zero_bias_grad(mod, bias: torch.Tensor) -> Optional[torch.Tensor]:
     slot = getattr(bias, "_slot", None)
     if slot is None:
         return torch.zeros(bias.shape, device=bias.device, dtype=torch.float32)
-    if not getattr(slot, "_static_zero", False):
-        slot.grad.zero_()  # once: nothing else ever writes this slot
-        slot._static_zero = True
+    done = mod.__dict__.setdefault("_zeroed_slots", {})
+    key = (id(slot.store), slot.index)
+    if done.get(key) != slot.grad.data_ptr():
+        slot.grad.zero_()  # once per buffer: nothing else ever writes this slot
+        done[key] = slot.grad.data_ptr()
     slot.store.mark_ready(slot.index)
     return None
 

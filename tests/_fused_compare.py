@@ -181,14 +181,21 @@ def run_three(base, stem, batch, monkeypatch, block_out=True, gamma_last=0.2, mu
         w = bstages["fp32"].get(ln)
         if w is not None and ln in bstages["fused"] and ln in bstages["module"]:
             out["bstage"][ln] = (rel(bstages["fused"][ln], w), rel(bstages["module"][ln], w))
+            out["bstage_fm"] = out.get("bstage_fm", {})
+            out["bstage_fm"][ln] = rel(bstages["fused"][ln], bstages["module"][ln])
     for ln in STAGES:
         w = stages["fp32"][ln]
         out["stage"][ln] = (rel(stages["fused"][ln], w), rel(stages["module"][ln], w))
         out["stage_fm"][ln] = rel(stages["fused"][ln], stages["module"][ln])
+    norms = sorted(gr[o:o + n_].norm().item() for o, n_ in store.segments())
+    med = norms[len(norms) // 2]
+    out["param_small"] = set()
     for (o, n_), name in zip(store.segments(), store.names):
         w = gr[o:o + n_]
         if w.norm().item() < 1e-8:
             continue
+        if w.norm().item() < 1e-3 * med:  # an fp32 gradient that is itself round-off
+            out["param_small"].add(name)
         out["param"][name] = (rel(gf[o:o + n_], w), rel(gm[o:o + n_], w))
         out["param_fm"][name] = rel(gf[o:o + n_], gm[o:o + n_])
     out["total_grad"] = (rel(gf, gr), rel(gm, gr))
@@ -197,29 +204,45 @@ def run_three(base, stem, batch, monkeypatch, block_out=True, gamma_last=0.2, mu
     return out
 
 
-# Bounds on the conditioned network (calibration on MI355X: tests/test_gpu_fused.py docstring).
-STAGE_TOL = 0.02       # relative L2 error of a stage output vs fp32
-PARAM_TOL = 0.02       # relative L2 error of one parameter's gradient vs fp32
-PARAM_SLACK = 0.0075   # ... or within this of the module path's own error (for the few
-                       # parameters whose gradient is itself tiny, e.g. β before a ReLU mask)
-BUFFER_TOL = 0.004     # running mean / var after one step
+# Bounds on the conditioned network, calibrated on MI355X (ResNet-50 CIFAR stem, batch 32 x 2
+# views; tools/fused_calib.py).  Forward stage outputs: 0.30 / 0.41 / 0.44 / 0.65 % from fp32 on
+# BOTH bf16 paths (fused / module within 2 % of each other); input gradients of the stages
+# 1.50 / 1.35 / 1.18 / 0.89 % on both (ratio 1.000-1.004); running statistics <= 0.09 %.  The
+# norms of these error tensors concentrate (millions of independent rounding errors), so the
+# fused path's error tracks the module path's to a fraction of a percent, and a defect that
+# adds a coherent component shows as a ratio: a 2 % error in one layer3 conv moved them by
+# +15 % (its input gradient) to +35 % (its forward output), and the running statistics of the
+# next BatchNorm 100x.  Per-parameter gradients are only checked grossly: each is a sum of
+# ~1e5 products whose rounding noise does not average out (7-10 % from fp32 for a conv weight
+# on both paths, 10-15 % apart from each other), and the biases of BatchNorms that feed a
+# BatchNorm through 1x1 convs have an fp32 gradient that is itself round-off.
+STAGE_ABS, STAGE_RATIO, STAGE_SLACK = 0.02, 1.10, 0.001
+BSTAGE_ABS, BSTAGE_RATIO, BSTAGE_SLACK = 0.045, 1.06, 0.0005
+BUFFER_RATIO, BUFFER_SLACK = 1.5, 0.002
+TOTAL_RATIO, TOTAL_SLACK = 1.25, 0.01
+PARAM_RATIO, PARAM_SLACK = 2.0, 0.05
 
 
 def violations(mt):
     """Every bound the fused path breaks (empty list = pass)."""
     bad = []
     for ln, (ef, em) in mt["stage"].items():
-        if ef > STAGE_TOL:
+        if ef > STAGE_ABS or ef > STAGE_RATIO * em + STAGE_SLACK:
             bad.append(("stage", ln, ef, em))
-    for name, (ef, em) in mt["param"].items():
-        if ef > PARAM_TOL and ef > em + PARAM_SLACK:
-            bad.append(("grad", name, ef, em))
-    ef, em = mt["total_grad"]
-    if ef > PARAM_TOL:
-        bad.append(("grad", "total", ef, em))
+    for ln, (ef, em) in mt["bstage"].items():
+        if ef > BSTAGE_ABS or ef > BSTAGE_RATIO * em + BSTAGE_SLACK:
+            bad.append(("input-grad", ln, ef, em))
     for name, (ef, em) in mt["buffers"].items():
-        if ef > BUFFER_TOL:
+        if ef > BUFFER_RATIO * em + BUFFER_SLACK:
             bad.append(("buffer", name, ef, em))
+    ef, em = mt["total_grad"]
+    if ef > TOTAL_RATIO * em + TOTAL_SLACK:
+        bad.append(("grad", "total", ef, em))
+    for name, (ef, em) in mt["param"].items():
+        if name in mt["param_small"]:
+            continue
+        if ef > PARAM_RATIO * em + PARAM_SLACK:
+            bad.append(("grad", name, ef, em))
     return bad
 
 
@@ -241,6 +264,7 @@ def summary(mt, top=6):
     return {"stage": {k: (round(a, 5), round(b, 5)) for k, (a, b) in mt["stage"].items()},
             "stage_fm": {k: round(v, 5) for k, v in mt["stage_fm"].items()},
             "bstage": {k: (round(a, 5), round(b, 5)) for k, (a, b) in mt["bstage"].items()},
+            "bstage_fm": {k: round(v, 5) for k, v in mt.get("bstage_fm", {}).items()},
             "fm_conv_q50_q90_max": _dist(fmc),
             "fm_worst": [(k, round(v, 5)) for k, v in fm[:top]],
             "conv_grad_q50_q90_max": (_dist([a for _, (a, b) in convs]),

@@ -170,10 +170,10 @@ def test_bn_apply_ss_and_finalize_table(ops, mode):
                                                        ("resnet50", True, 64, False),
                                                        ("resnet50", True, 64, True)])
 def test_fused_stages_match_fp32(base, stem, batch, block_out, monkeypatch):
-    """The fused executor vs fp32 torch on a well-conditioned network (tests/_fused_compare.py:
-    damped residual branches, projection loss): every stage output, every parameter gradient and
-    every running statistic within absolute bounds of the fp32 run of the same weights.  The
-    module path is computed alongside as the bf16 floor of the same network (printed)."""
+    """The fused executor vs fp32 torch and vs the per-module bf16 path on a well-conditioned
+    network (tests/_fused_compare.py: damped residual branches, ReLU inputs away from zero,
+    a projection loss on the backbone features): stage outputs, stage input gradients, running
+    statistics and parameter gradients within the calibrated bounds of _fused_compare.py."""
     from _fused_compare import run_three, summary, violations
     mt = run_three(base, stem, batch, monkeypatch, block_out=block_out)
     print("FUSED-CHECK", base, batch, block_out, summary(mt))
@@ -182,16 +182,17 @@ def test_fused_stages_match_fp32(base, stem, batch, block_out, monkeypatch):
         assert (dual, outs) == (nblk - 1, 1), (dual, outs)
     else:
         assert (dual, outs) == (0, nblk), (dual, outs)
+    assert mt["bstage"] and len(mt["stage"]) == 4
     bad = violations(mt)
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("mutate", [("fwd", "layer3.1", 1), ("dgrad", "layer3.1", 1),
-                                    ("fwd", "layer3.0", 2)])
+@pytest.mark.parametrize("mutate", [("fwd", "layer3.1", 1), ("fwd", "layer3.0", 2),
+                                    ("dgrad", "layer3.1", 1), ("dgrad", "layer2.2", 0)])
 def test_fused_check_catches_two_percent_defect(mutate, monkeypatch):
-    """Sensitivity of the check above: one layer3 conv of the fused executor made 2 % wrong
-    (its forward output after the BatchNorm statistics were taken, or its input gradient) must
-    break at least one bound."""
+    """Sensitivity of the check above: one conv of the fused executor made 2 % wrong — its
+    forward output after the BatchNorm statistics were taken (what its consumers read), or its
+    input gradient — must break at least one bound (measured margins: _fused_compare.py)."""
     from _fused_compare import run_three, summary, violations
     mt = run_three("resnet50", True, 32, monkeypatch, mutate=mutate)
     bad = violations(mt)

@@ -39,7 +39,7 @@ def _reference(m, x, R, S):
     W2 = s.linear2.weight.detach().clone().requires_grad_()
     b2 = (s.linear2.bias.detach().clone().requires_grad_() if s.linear2.bias is not None
           else None)
-    xf = x.float().clone().requires_grad_()
+    xf = x.detach().float().requires_grad_()
     y1 = xf @ W1.t() + b1
     n = x.shape[0] // S
     ys, means, vars_ = [], [], []
@@ -95,7 +95,7 @@ def test_fused_head_matches_fp32(H, D, nonlinear):
     # b1 in front of a BatchNorm: the exact gradient is 0 (the fp32 reference's is round-off)
     assert bool((s.linear1.bias.grad == 0).all())
     assert g_ref["linear1.bias"].abs().max().item() < 1e-3 * g_ref["linear1.weight"].abs().max().item()
-    assert _rel(s.bn1.running_mean, rm_ref) < 1e-3 and _rel(s.bn1.running_var, rv_ref) < 1e-3
+    assert _rel(s.bn1.running_mean, rm_ref) < 3e-3 and _rel(s.bn1.running_var, rv_ref) < 3e-3
     assert int(s.bn1.num_batches_tracked) == S
 
 
@@ -103,13 +103,15 @@ def _head_kernels(m, x, R, S, fused):
     """Kernel launches of one head forward + backward (a captured graph's kernel nodes)."""
     from simclr_amd.runtime.graph_exec import StreamReplay
     m.use_fused = fused
+    R16 = R.to(torch.bfloat16)
     for _ in range(2):  # eager: autotune, plans
         x.grad = None
-        (m(x, segments=S).float() * R).sum().backward()
+        m(x, segments=S).backward(R16)
     torch.cuda.synchronize()
+    x.grad = None
     g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g):
-        (m(x, segments=S).float() * R).sum().backward()
+        m(x, segments=S).backward(R16)
     g.instantiate()
     st = StreamReplay(g, max_streams=1).stats()
     g.replay()

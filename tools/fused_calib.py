@@ -10,7 +10,7 @@ class MP:
         self.undo=[]
 for loss in ("energy", "projection"):
     pass
-for loss in ("energy",):
+for loss in ("projection",):
     for mut in (None, ("dgrad", "layer3.1", 1), ("fwd", "layer3.1", 1), ("fwd", "layer3.0", 2), ("dgrad", "layer2.2", 0)):
         mp = MP()
         mt = run_three("resnet50", True, 32, mp, block_out=True, mutate=mut, loss=loss)
