@@ -8,6 +8,7 @@ implemented here as Linear(F,F) → BN1d → ReLU → Linear(F,C), mirroring the
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 
 import torch
@@ -53,7 +54,8 @@ class _MLP(nn.Module):
         return getattr(self, self._attr)
 
     # the fused GEMM-BN-GEMM schedule (models/head_fused.py) for eligible training batches
-    use_fused = True
+    # (SIMCLR_FUSED_HEAD=0: the per-op head, for A/B attribution)
+    use_fused = os.environ.get("SIMCLR_FUSED_HEAD", "1") != "0"
 
     def forward(self, x: torch.Tensor, segments: int = 1) -> torch.Tensor:
         s = self._seq
