@@ -521,6 +521,10 @@ void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t 
   if (mode == 0) {
     TORCH_CHECK(stats.has_value() && stats->numel() >= 2 * S * C, "bn_reduce_fused: stats");
     q.stats = f32w(*stats, "stats");
+    // optional: the local dβ = Σ_s Σg, dγ = Σ_s Σg·x̂ of a BatchNorm backward's partials (the
+    // distributed path all-reduces `stats` for the input-gradient coefficients afterwards)
+    q.dgamma = optf32w(dgamma, "dgamma");
+    q.dbeta = optf32w(dbeta, "dbeta");
   } else if (mode == 1) {
     TORCH_CHECK(mi.has_value() && mi->numel() >= 2 * S * C, "bn_reduce_fused: mi");
     q.mi = f32w(*mi, "mi");

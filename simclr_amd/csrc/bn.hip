@@ -392,6 +392,8 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
     if (p.mode == 0) {
       p.stats[sg * C + c] = s1;
       p.stats[S * C + sg * C + c] = s2;
+      db += s1;  // written only when dβ / dγ outputs are given (BN-backward partials)
+      dg += s2;
     } else if (p.mode == 1) {
       const float mean = s1 / p.count;
       float var = s2 / p.count - mean * mean;
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
   if (p.mode == 1) {
     if (p.running_mean) p.running_mean[c] = rm;
     if (p.running_var) p.running_var[c] = rv;
-  } else if (p.mode == 2) {
+  } else {
     if (p.dgamma) p.dgamma[c] = dg;
     if (p.dbeta) p.dbeta[c] = db;
   }

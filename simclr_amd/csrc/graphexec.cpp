@@ -63,11 +63,6 @@ struct Exec {
   hipEvent_t fork = nullptr;
   std::vector<hipEvent_t> joins;
   int nstreams = 1;
-  // priority mode: stream 0 (the chain that carries the step's critical path) is an own
-  // highest-priority stream instead of the caller's, so the command processor dispatches its
-  // workgroups ahead of the side streams' whenever both have work queued
-  hipStream_t hi = nullptr;
-  hipEvent_t hi_join = nullptr;
   int64_t counts[8] = {0};  // per NodeKind (kKernel..kEvWait) and the number of waits
   ~Exec() {
     for (auto& nd : nodes)
@@ -76,8 +71,6 @@ struct Exec {
     for (auto e : joins) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
     for (size_t i = 1; i < streams.size(); ++i) (void)hipStreamDestroy(streams[i]);
-    if (hi_join) (void)hipEventDestroy(hi_join);
-    if (hi) (void)hipStreamDestroy(hi);
   }
 };
 
@@ -104,7 +97,7 @@ hipGraphExec_t single_node_exec(hipGraph_t g, hipGraphNode_t node) {
   return e;
 }
 
-int64_t gexec_create(int64_t graph_handle, int64_t max_streams, int64_t priority) {
+int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
   TORCH_CHECK(graph_handle != 0, "graphexec: null graph");
   TORCH_CHECK(max_streams >= 1 && max_streams <= 8, "graphexec: 1..8 streams");
   hipGraph_t g = reinterpret_cast<hipGraph_t>(graph_handle);
@@ -206,7 +199,8 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams, int64_t priority
   }
   ex->nstreams = used;
   // the busiest chain (the step's critical path: the dgrad / BatchNorm chain, not the weight
-  // gradients beside it) becomes stream 0 — the caller's stream, or the high-priority one
+  // gradients beside it) becomes stream 0, the caller's stream.  (Replaying that chain on a
+  // highest-priority stream instead was measured 27.9 vs 21.5 ms/step: rejected, r5 log.)
   {
     std::vector<int> cnt(used, 0);
     for (const Node& nd : ex->nodes) cnt[nd.stream]++;
@@ -275,12 +269,6 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams, int64_t priority
     ex->joins.push_back(e);
   }
   GX_CHECK(hipEventCreateWithFlags(&ex->fork, hipEventDisableTiming));
-  if (priority > 0) {
-    int least = 0, greatest = 0;
-    GX_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    GX_CHECK(hipStreamCreateWithPriority(&ex->hi, hipStreamNonBlocking, greatest));
-    GX_CHECK(hipEventCreateWithFlags(&ex->hi_join, hipEventDisableTiming));
-  }
   return reinterpret_cast<int64_t>(ex.release());
 }
 
@@ -323,10 +311,9 @@ void issue(const Node& nd, hipStream_t st) {
 void gexec_replay(int64_t h) {
   Exec* ex = as_exec(h);
   hipStream_t cur = at::hip::getCurrentHIPStream().stream();
-  ex->streams[0] = ex->hi ? ex->hi : cur;
-  if (ex->nstreams > 1 || ex->hi) {
+  ex->streams[0] = cur;
+  if (ex->nstreams > 1) {
     GX_CHECK(hipEventRecord(ex->fork, cur));
-    if (ex->hi) GX_CHECK(hipStreamWaitEvent(ex->hi, ex->fork, 0));
     for (int k = 1; k < ex->nstreams; ++k) GX_CHECK(hipStreamWaitEvent(ex->streams[k], ex->fork, 0));
   }
   for (const Node& nd : ex->nodes) {
@@ -338,10 +325,6 @@ void gexec_replay(int64_t h) {
   for (int k = 1; k < ex->nstreams; ++k) {
     GX_CHECK(hipEventRecord(ex->joins[k - 1], ex->streams[k]));
     GX_CHECK(hipStreamWaitEvent(cur, ex->joins[k - 1], 0));
-  }
-  if (ex->hi) {
-    GX_CHECK(hipEventRecord(ex->hi_join, ex->hi));
-    GX_CHECK(hipStreamWaitEvent(cur, ex->hi_join, 0));
   }
 }
 
@@ -371,7 +354,7 @@ void gexec_destroy(int64_t h) {
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(simclr_amd, m) {
-  m.def("gexec_create(int graph, int max_streams, int priority=0) -> int", &gexec_create);
+  m.def("gexec_create(int graph, int max_streams) -> int", &gexec_create);
   m.def("gexec_replay(int handle) -> ()", &gexec_replay);
   m.def("gexec_stats(int handle) -> int[]", &gexec_stats);
   m.def("gexec_streams(int handle) -> int[]", &gexec_streams);

@@ -331,10 +331,9 @@ class FusedStages:
             return ("local", bn, partial, nblk_seg, bs, st.ipc)
         dev = partial.device
         sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-        ops.bn_reduce_fused(partial, nblk_seg, S, C, 0, sums)
-        scratch = torch.empty((3 * S * C,), device=dev, dtype=torch.float32)
-        self._deliver_bn_grads(bn, lambda dg, db: ops.bn_bwd_finalize(
-            sums, bs.mi, bn.weight.detach(), S, C, bs.count, dg, db, scratch))
+        # one launch: the local sums (all-reduced below) and dγ, dβ from them
+        self._deliver_bn_grads(bn, lambda dg, db: ops.bn_reduce_fused(
+            partial, nblk_seg, S, C, 0, sums, dgamma=dg, dbeta=db))
         work = dist.all_reduce(sums, group=st.stats_group, async_op=True)
         return ("dist", bn, sums, work, bs)
 

@@ -115,8 +115,7 @@ class BatchNormHipFn(torch.autograd.Function):
             # dγ, dβ from the LOCAL sums (the data-parallel reducer sums them across ranks,
             # as SyncBatchNorm + DDP do); the input gradient needs the global sums
             sums = torch.empty((2 * S * C,), device=dev, dtype=torch.float32)
-            ops.bn_reduce_fused(partial, nblk, S, C, 0, sums)
-            ops.bn_bwd_finalize(sums, mi, weight.detach(), S, C, count, dgamma, dbeta, coef)
+            ops.bn_reduce_fused(partial, nblk, S, C, 0, sums, dgamma=dgamma, dbeta=dbeta)
             _allreduce(sums, st)
             ops.bn_bwd_finalize(sums, mi, weight.detach(), S, C, count, None, None, coef)
         if gslot is not None:

@@ -13,9 +13,6 @@ There is no reference counterpart (the reference issues every op eagerly through
 """
 from __future__ import annotations
 
-import os
-from typing import Optional
-
 import torch
 
 from ..ops import _ext
@@ -28,17 +25,11 @@ class StreamReplay:
     """Native multi-stream issue of the nodes of ``graph`` (a ``CUDAGraph(keep_graph=True)``
     after ``capture_end``).  The CUDAGraph object must stay alive while this is used."""
 
-    def __init__(self, graph: torch.cuda.CUDAGraph, max_streams: int = 3,
-                 priority: Optional[int] = None):
+    def __init__(self, graph: torch.cuda.CUDAGraph, max_streams: int = 3):
         _ext.require()
         self._ops = torch.ops.simclr_amd
         self.graph = graph
-        if priority is None:
-            priority = int(os.environ.get("SIMCLR_REPLAY_PRIORITY", "0"))
-        # priority 1: the critical-path chain (stream 0) replays on a highest-priority stream
-        self.priority = priority
-        self.handle = int(self._ops.gexec_create(int(graph.raw_cuda_graph()), int(max_streams),
-                                                 int(priority)))
+        self.handle = int(self._ops.gexec_create(int(graph.raw_cuda_graph()), int(max_streams)))
 
     def stats(self) -> dict:
         return dict(zip(STAT_NAMES, (int(v) for v in self._ops.gexec_stats(self.handle))))

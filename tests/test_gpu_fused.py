@@ -231,6 +231,14 @@ def test_bn_reduce_fused_matches_three_launch_path(ops, C, nblk, S):
         dg0, db0 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
         dg1, db1 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
         ops.bn_bwd_finalize(stats, mi0, gamma, S, C, count, dg0, db0, coef0)
+        # mode 0 with dγ, dβ (the distributed backward: local sums + parameter gradients in one
+        # launch, the sums all-reduced afterwards)
+        st3 = torch.empty(2 * S * C, device=DEV)
+        dg2, db2 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        ops.bn_reduce_fused(part, nblk, S, C, 0, st3, dgamma=dg2, dbeta=db2)
+        assert torch.allclose(st3, stats, rtol=1e-5, atol=1e-4)
+        assert torch.allclose(dg2, dg0, rtol=1e-4, atol=1e-3)
+        assert torch.allclose(db2, db0, rtol=1e-4, atol=1e-3)
         ops.bn_reduce_fused(part, nblk, S, C, 2, None, count, 0.0, 0.0, None, None, mi0, None,
                             gamma, None, None, dg1, db1, coef1)
         for u, v in ((coef1, coef0), (dg1, dg0), (db1, db0)):
