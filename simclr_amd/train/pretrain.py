@@ -136,7 +136,7 @@ class Trainer:
         self.guard.check(self.opt.host_step)
         return loss
 
-    def capture(self, x: torch.Tensor, warmup: int = 2, streams: int = 3) -> None:
+    def capture(self, x: torch.Tensor, warmup: int = 2, streams: int = -1) -> None:
         """Capture one full training step into a hipGraph (after ``warmup`` eager steps) and
         build the native multi-stream executor over its nodes (``streams`` > 0; kept as
         ``self.sreplay``, selected by ``replay_mode = "streams"``)."""
@@ -165,6 +165,10 @@ class Trainer:
         g.instantiate()
         self.graph = g
         self.sreplay = None
+        if streams < 0:
+            # main chain, weight-gradient stream, downsample branch (+ the gradient all-reduce's
+            # chain at N > 1); at most the 4 hardware queues a process gets (GPU_MAX_HW_QUEUES)
+            streams = 4 if self.st.comm else 3
         if streams > 0:
             from ..runtime.graph_exec import StreamReplay
             try:
