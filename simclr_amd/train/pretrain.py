@@ -12,7 +12,9 @@ MI355X step (``Trainer.step``), identical math:
   backward with gradients written into the flat fp32 buffer and bucketed RCCL all-reduces on a
   comm stream → ``lr_step`` + fused LARS (no host sync anywhere in the step).
 Optionally the whole step (fwd + bwd + optimizer) is captured once into a hipGraph and replayed
-(``runtime.hip_graph=true``) to remove per-kernel launch overhead.
+(``runtime.hip_graph=true``) to remove per-kernel launch overhead: by the native multi-stream
+executor over the captured nodes (``runtime.replay=streams``, runtime/graph_exec.py) or by
+``hipGraphLaunch`` (``runtime.replay=graph``).
 """
 from __future__ import annotations
 
@@ -243,6 +245,7 @@ def pretrain(cfg) -> dict:
                 prof = _start_profiler()
             if use_graph and tr.graph is None:
                 tr.capture(x)
+                tr.replay_mode = str(cfg_get(cfg, "runtime.replay", "streams"))
             loss = tr.step(x)
             nsteps += 1
             step_global += 1
