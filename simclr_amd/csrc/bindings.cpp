@@ -313,9 +313,13 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
     TORCH_CHECK(dp_coef.has_value() && dp_coef->numel() >= 3 * dp_S * g.N, "wgrad: dp_coef [3][S][N]");
     const int64_t iters = (M + 63) / 64;
     const int64_t ips = (iters + splits - 1) / splits;
-    TORCH_CHECK(dp_seg_rows > 0 && M % dp_seg_rows == 0 && dp_seg_rows % (ips * 64) == 0 &&
-                    M / dp_seg_rows == dp_S,
-                "wgrad dY prologue: every split must lie inside one segment");
+    // a split may straddle at most one segment boundary (the kernel holds two coefficient sets)
+    TORCH_CHECK(dp_seg_rows > 0 && M % dp_seg_rows == 0 && M / dp_seg_rows == dp_S &&
+                    (dp_S <= 2 || dp_seg_rows % (ips * 64) == 0) && dp_seg_rows % 64 == 0,
+                "wgrad dY prologue: 64-row segments, and every split inside one segment when "
+                "there are more than two");
+    TORCH_CHECK(!wgrad_variant_glds((int)variant),
+                "wgrad dY prologue: register-staged variants only");
     f.dY2 = bf(*dY2, "dY2");
     f.dp_coef = f32(*dp_coef, "dp_coef");
     f.dp_seg_rows = (int)dp_seg_rows;

@@ -1395,20 +1395,28 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 
   struct Stage {
     u32x4 rd[DCH], rx[XCH], rd2[DCH];
-    bool dok[DCH], xok[XCH], xseg[XCH];
+    bool dok[DCH], xok[XCH], xseg[XCH], dseg[DCH];
   };
   Stage S0, S1;
-  float dA[8], dB[8], dD[8];
+  // dY prologue coefficients of the split's first segment and of the next one: with at most two
+  // segments (views) a split may straddle the boundary, each dY row picks its set (host-checked:
+  // dp_S <= 2, or every split inside one segment)
+  float dA[8], dB[8], dD[8], dA1[8], dB1[8], dD1[8];
   const __amdgpu_buffer_rsrc_t rd2_src = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(DPRO ? p.dY2 : p.dY), (short)0, (int)p.dy_bytes, 0x00020000);
+  const int dseg0 = DPRO ? (split * p.iters_per_split * 64) / p.dp_seg_rows : 0;
+  const int dseg_next_row = (dseg0 + 1) * p.dp_seg_rows;  // first row of the next segment
   if (DPRO) {
-    const int dseg = (split * p.iters_per_split * 64) / p.dp_seg_rows;
     const int cc = dcol_ok ? dcol : 0;
+    const int s1 = dseg0 + 1 < p.dp_S ? dseg0 + 1 : dseg0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      dA[e] = p.dp_coef[dseg * p.N + cc + e];
-      dB[e] = p.dp_coef[(p.dp_S + dseg) * p.N + cc + e];
-      dD[e] = p.dp_coef[(2 * p.dp_S + dseg) * p.N + cc + e];
+      dA[e] = p.dp_coef[dseg0 * p.N + cc + e];
+      dB[e] = p.dp_coef[(p.dp_S + dseg0) * p.N + cc + e];
+      dD[e] = p.dp_coef[(2 * p.dp_S + dseg0) * p.N + cc + e];
+      dA1[e] = p.dp_coef[s1 * p.N + cc + e];
+      dB1[e] = p.dp_coef[(p.dp_S + s1) * p.N + cc + e];
+      dD1[e] = p.dp_coef[(2 * p.dp_S + s1) * p.N + cc + e];
     }
   }
   constexpr bool pro = PRO;
@@ -1460,6 +1468,7 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
       if (DPRO) {
         st.rd2[j] = __builtin_amdgcn_raw_buffer_load_b128(rd2_src, ok ? doff[j] : p.dy_bytes, 0, 0);
         st.dok[j] = ok;
+        st.dseg[j] = m >= dseg_next_row;
       }
       doff[j] += dstep;
     }
@@ -1490,7 +1499,9 @@ __global__ __launch_bounds__(256, (BCO * BKK > 128 * 128) ? 1 : 2) void wgrad_tn
 #pragma unroll
     for (int j = 0; j < DCH; ++j)
       *(u32x4*)(Ds + buf * 64 * SD + (drow + RD * j) * SD + tr_swz<BCO>(drow + RD * j, dch * 8)) =
-          DPRO ? bnbwd8(st.rd[j], st.rd2[j], dA, dB, dD, st.dok[j]) : st.rd[j];
+          DPRO ? (st.dseg[j] ? bnbwd8(st.rd[j], st.rd2[j], dA1, dB1, dD1, st.dok[j])
+                             : bnbwd8(st.rd[j], st.rd2[j], dA, dB, dD, st.dok[j]))
+               : st.rd[j];
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       u32x4 v = st.rx[j];
@@ -3182,6 +3193,9 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     default: launch_wgrad<64, 64, 2, 2>(a, s); break;
   }
   const int K = a.K;
+  // one split writing its slab straight into the output (the caller passed partial == out): the
+  // slab IS the [N][K] fp32 gradient, no reduction launch
+  if (splits == 1 && partial == out && Creal == g.C && beta == 0.f) return;
   const size_t n4 = (size_t)a.N * K / 4;
   int sstride = 1, count = splits;
   constexpr int GROUP = 16;

@@ -14,12 +14,14 @@ runs (S = 2 view segments, statistics per segment, all-reduced across ranks)::
                                          prologue: relu(bn(y1)) is never written to HBM
               (+ the transposed weights W1ᵀ, W2ᵀ for the backward: one batched launch)
     backward  g = (dz·W2)·[bn(y1) > 0]   dgrad 2, epilogue: ReLU mask + Σg, Σg·x̂ partials
-              dW2 = dzᵀ·relu(bn(y1))     weight gradient, the BN + ReLU in the X prologue
+              dW2 = dzᵀ·relu(bn(y1))     weight gradient, the BN + ReLU in the X prologue, one
+                                         split written straight into the flat gradient
               finalize                   dγ, dβ (flat gradient buffer) and the input-gradient
                                          coefficients; cross-GPU combine here
               dx = (A·g + B·y1 + D)·W1   dgrad 1, the BN backward in the A-operand prologue:
                                          the BN's input gradient is never written to HBM
               dW1 = (A·g + B·y1 + D)ᵀ·x  weight gradient, the same prologue on its dY operand
+                                         (per-row view segment), one split, no reduction
 
 The gradient of b1 is exactly zero: a bias in front of a BatchNorm cancels in (y − mean(y)),
 so dL/db1 = Σ_rows dL/dy1 = 0 for every view over the global batch (the reference's autograd
@@ -33,7 +35,7 @@ from typing import Optional
 import torch
 
 from ..ops import _ext
-from ..ops.conv_hip import igemm_choose, igemm_launch, run_wgrad
+from ..ops.conv_hip import igemm_choose, igemm_launch
 from ..parallel import state as pstate
 
 
@@ -51,6 +53,30 @@ def _w16(weight: torch.Tensor) -> torch.Tensor:
 def _bnops():
     from .fused import FusedStages
     return FusedStages.__new__(FusedStages)  # the stateless BatchNorm helpers of the executor
+
+
+def _wgrad_direct(ops, dY, X, out, geom, creal, pro=None, dpro=None):
+    """Weight gradient in ONE split written straight into ``out`` (no split-reduction launch):
+    the head's GEMMs have 1,024 rows, so the 128 x 128 output tiles already give up to 256
+    blocks.  ``pro = (sc, sh, seg_rows, relu, S)``: X-operand BN + ReLU; ``dpro = (dY2, coef,
+    seg_rows, S)``: dY-operand BatchNorm backward (register-staged variants, which take the
+    per-row view segment)."""
+    from ..ops import tuning
+    psc, psh, pseg, prelu, pS = pro if pro is not None else (None, None, 0, False, 1)
+    dY2, dcoef, dseg, dS = dpro if dpro is not None else (None, None, 0, 1)
+    key = ("wgrad1split", tuple(geom), creal, psc is not None, dpro is not None)
+
+    def launch(v, o):
+        ops.wgrad(dY, X, o, o, geom, 1, creal, 0.0, psc, psh, pseg, prelu, pS, v, dY2, dcoef,
+                  dseg, dS)
+
+    v = tuning.cached(key)
+    if v is None:
+        cands = [v for v in range(ops.wgrad_nvariants())
+                 if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)
+                 and (dpro is None or not ops.wgrad_variant_glds(v))]
+        v = tuning.pick(key, cands, 0, lambda vv: launch(vv, torch.empty_like(out)))
+    launch(v, out)
 
 
 def _deliver(param: torch.Tensor, compute) -> Optional[torch.Tensor]:
@@ -151,8 +177,8 @@ class MLPHeadFn(torch.autograd.Function):
         h = bnx._bn_bwd_start(ops, bn, part, nb, bs, S, st)
         # dW2 = dzᵀ · relu(bn(y1)) (X prologue), independent of the BN backward
         pro = (bs.ss[0], bs.ss[1], seg, True, S)
-        gw2 = _deliver(lin2.weight, lambda o: run_wgrad(ops, dzc, y1, o.view(D, 1, 1, H),
-                                                        _geom(M, H, D), H, pro=pro))
+        gw2 = _deliver(lin2.weight, lambda o: _wgrad_direct(ops, dzc, y1, o.view(D, 1, 1, H),
+                                                            _geom(M, H, D), H, pro=pro))
         gb2 = None
         if ctx.has_b2:
             gb2 = _deliver(lin2.bias, lambda o: ops.colsum(dzc, o, 0.0))
@@ -167,9 +193,9 @@ class MLPHeadFn(torch.autograd.Function):
             v = igemm_choose(ops, gm, wt1, dx, gx, bnb=bpro)
             igemm_launch(ops, gm, wt1, dx, gx, v, bnb=bpro)
         # dW1 = daᵀ · x, the same prologue on the dY operand
-        gw1 = _deliver(lin1.weight, lambda o: run_wgrad(ops, gm, xc, o.view(H, 1, 1, K),
-                                                        _geom(M, K, H), K,
-                                                        dpro=(y1, coef, seg, S)))
+        gw1 = _deliver(lin1.weight, lambda o: _wgrad_direct(ops, gm, xc, o.view(H, 1, 1, K),
+                                                            _geom(M, K, H), K,
+                                                            dpro=(y1, coef, seg, S)))
         gb1 = _zero_bias_grad(mod, lin1.bias)
         return dx, gw1, gb1, None, None, gw2, gb2, None, None
 

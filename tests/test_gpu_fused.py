@@ -396,3 +396,33 @@ def test_patch_kernels_bn_apply_prologue(ops, H, C, Co):
     assert 17 in outs, "wgrad_patch did not admit the X prologue"
     for v, o in outs.items():
         assert _rel(o, wref) < 1e-2, v
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+def test_wgrad_dy_prologue_split_straddles_views(ops, splits):
+    """The register-staged weight gradient with the BatchNorm-backward dY prologue, with splits
+    that straddle the two views' boundary (each dY row takes its own view's coefficients), ==
+    the weight gradient of the materialised da = A·dY + B·a + D (and both vs fp32); one split
+    writes the output directly (partial == out, no reduction)."""
+    torch.manual_seed(21)
+    S, N, H, Ci, Co = 2, 16, 8, 128, 256
+    M = N * H * H
+    g = _bf(torch.randn(N, H, H, Co, device=DEV))
+    a = _bf(torch.randn(N, H, H, Co, device=DEV))
+    x = _bf(torch.randn(N, H, H, Ci, device=DEV))
+    coef = torch.randn(3 * S * Co, device=DEV) * 0.5
+    da = torch.empty_like(a)
+    ops.bn_bwd_apply(g, None, a, coef, S, False, da, None)
+    geom = [N, H, H, Ci, H, H, 1, 1, 1, 1, 1, 1, 0, 0, Co, H, H, 1, 1, 0, 0, Co]
+    ref = (da.float().reshape(M, Co).t() @ x.float().reshape(M, Ci))
+    seen = 0
+    for v in range(ops.wgrad_nvariants()):
+        if ops.wgrad_variant_glds(v) or not ops.wgrad_variant_ok(v, geom, False, True):
+            continue
+        out = torch.full((Co, Ci), float("nan"), device=DEV)
+        part = out if splits == 1 else torch.empty(splits * Co * Ci, device=DEV)
+        ops.wgrad(g, x, part, out, geom, splits, Ci, 0.0, None, None, 0, False, 1, v, a, coef,
+                  M // S, S)
+        assert _rel(out, ref) < 1e-2, (v, splits)
+        seen += 1
+    assert seen >= 2

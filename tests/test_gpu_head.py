@@ -120,11 +120,11 @@ def _head_kernels(m, x, R, S, fused):
 
 
 def test_fused_head_cuts_launches():
-    """The fused head (K6) issues at most 70 % of the kernels of the per-op head path for the
+    """The fused head (K6) issues at most 60 % of the kernels of the per-op head path for the
     same forward + backward (bound to a flat parameter store, as in training).  Measured on
-    MI355X: 11 vs 17 (forward: GEMM, finalize, GEMM, one batched weight transpose; backward:
-    dgrad + mask/partials, weight gradient + split reduce, finalize, dgrad with the
-    BN-backward prologue, weight gradient + split reduce)."""
+    MI355X: 9 vs 17 (forward: GEMM, finalize, GEMM, one batched weight transpose; backward:
+    dgrad + mask/partials, one-split weight gradient, finalize, dgrad with the BN-backward
+    prologue, one-split weight gradient)."""
     from simclr_amd.parallel import state as pstate
     from simclr_amd.parallel.flat import FlatParamStore
     pstate.reset()
@@ -137,4 +137,4 @@ def test_fused_head_cuts_launches():
     k_fused = _head_kernels(m, x, R, S, True)
     k_ops = _head_kernels(m, x, R, S, False)
     print("head kernels fused / per-op:", k_fused, k_ops)
-    assert 10 * k_fused <= 7 * k_ops, (k_fused, k_ops)
+    assert k_fused <= 9 and 10 * k_fused <= 6 * k_ops, (k_fused, k_ops)
