@@ -24,6 +24,7 @@
 // out-of-range offset returns zeros, so conv padding / M and K tails need no branches around the
 // loads.  Tiles: BM x BN x 64, 256 threads (4 waves), mfma_f32_16x16x32_bf16, LDS double buffer
 // with an XOR chunk swizzle (cdna_hip_programming.md T2), XCD-aware block remap (T1).
+#include <cstring>
 #include "common.h"
 #include "kernels.h"
 
@@ -1152,6 +1153,7 @@ struct WgradArgs {
   const uint16_t* dY2;
   const float* dp_coef;
   int dp_seg_rows, dp_S;
+  size_t slab_stride;  // floats between split slabs (N*K; 0 only in the attribution experiment)
 };
 
 // Weight-gradient MFMA shape: 16 = v_mfma_f32_16x16x32_bf16 (f32x4 accumulators), 32 =
@@ -1290,7 +1292,7 @@ __device__ __forceinline__ void wgrad_store_at(
   constexpr int FM = TCO / MF, FN = TKK / MF;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, li = lane & 15;
-  float* out = p.partial + (size_t)split * p.N * p.K;
+  float* out = p.partial + (size_t)split * p.slab_stride;
   // a whole wave tile (the usual case) stores without per-element guards: the guarded loop
   // becomes one exec-mask branch per store (FM x FN x 16 of them per thread at 32x32)
   const bool full = cw + TCO <= p.N && kw + TKK <= p.K;
@@ -2305,7 +2307,7 @@ __global__ __launch_bounds__(576, 1) void wgrad_patch(WgradArgs p) {
     }
   }
   // partial[split][co][tap * C + ci]
-  float* out = p.partial + (size_t)split * p.N * p.K;
+  float* out = p.partial + (size_t)split * p.slab_stride;
 #pragma unroll
   for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
@@ -3136,6 +3138,19 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   a.pro_relu = f.pro_relu; a.pro_S = f.pro_S > 0 ? f.pro_S : 1;
   a.dY2 = f.dY2; a.dp_coef = f.dp_coef; a.dp_seg_rows = f.dp_seg_rows > 0 ? f.dp_seg_rows : a.M;
   a.dp_S = f.dp_S > 0 ? f.dp_S : 1;
+  a.slab_stride = (size_t)a.N * a.K;
+  // attribution experiment (bench.py / tools only; refused by the training entry points):
+  // SIMCLR_EXPERIMENT_WGRAD_SLABS=noreduce skips the split reductions, =alias also makes every
+  // split write slab 0 (the weight gradients are garbage; what remains is the step without the
+  // split-slab traffic)
+  static const int slab_exp = [] {
+    const char* e = getenv("SIMCLR_EXPERIMENT_WGRAD_SLABS");
+    if (!e) return 0;
+    if (!strcmp(e, "noreduce")) return 1;
+    if (!strcmp(e, "alias")) return 2;
+    return 0;
+  }();
+  if (slab_exp == 2) a.slab_stride = 0;
   if (variant < 0 || variant >= wgrad_num_variants()) variant = wgrad_default_variant(g.N);
   if (!wgrad_variant_ok(variant, g, a.pro_sc != nullptr, a.dY2 != nullptr)) {
     fprintf(stderr, "wgrad: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
@@ -3196,6 +3211,7 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   // one split writing its slab straight into the output (the caller passed partial == out): the
   // slab IS the [N][K] fp32 gradient, no reduction launch
   if (splits == 1 && partial == out && Creal == g.C && beta == 0.f) return;
+  if (slab_exp != 0) return;
   const size_t n4 = (size_t)a.N * K / 4;
   int sstride = 1, count = splits;
   constexpr int GROUP = 16;

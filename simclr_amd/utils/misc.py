@@ -61,7 +61,7 @@ class MetricsWriter:
 
 # attribution knobs that change the math (bench / tools only): a leftover export in a training
 # shell would silently train a wrong model
-EXPERIMENT_KNOBS = ("SIMCLR_SKIP_WGRAD",)
+EXPERIMENT_KNOBS = ("SIMCLR_SKIP_WGRAD", "SIMCLR_EXPERIMENT_WGRAD_SLABS")
 
 
 def refuse_experiment_knobs(where: str) -> None:
