@@ -132,6 +132,8 @@ class FusedStages:
     executor); the class attribute ``BLOCK_OUT_PROLOGUE`` is the default of new executors."""
 
     BLOCK_OUT_PROLOGUE = True
+    # SIMCLR_FUSED_STEM=0: the stem stays on the per-module path (A/B attribution)
+    STEM_FUSED = os.environ.get("SIMCLR_FUSED_STEM", "1") != "0"
 
     def __init__(self, resnet: torch.nn.Module, segments: int = 2):
         from .resnet import BasicBlock, Bottleneck
@@ -186,6 +188,22 @@ class FusedStages:
         self._wt_cache = {}
         self._wt_table = None
         self._wt_ready = False
+        # the stem (conv1 + bn1 + ReLU, when no max-pool follows) inside the executor: its BatchNorm
+        # backward partials come from layer1.0's conv1 dgrad epilogue (mode 4, like every block
+        # boundary) and its weight gradient applies the BN backward in the dY prologue — no
+        # separate reduce pass over the 1024 x 32 x 32 x 64 stem activation, no materialised
+        # input gradient (stem_forward / backward)
+        self.stem_fused = type(self).STEM_FUSED
+        self.stem = None
+        self._stem_block = None
+        from .resnet import _Identity
+        if isinstance(getattr(resnet, "maxpool", None), _Identity):
+            c1 = resnet.conv1
+            k = c1.kernel_size[0] if isinstance(c1.kernel_size, tuple) else c1.kernel_size
+            st_ = c1.stride[0] if isinstance(c1.stride, tuple) else c1.stride
+            pd = c1.padding[0] if isinstance(c1.padding, tuple) else c1.padding
+            self.stem = _ConvSpec(c1, resnet.bn1, st_, k, pd)
+            self._stem_block = _BlockSpec([self.stem], None, "stem")
         self.blocks: List[_BlockSpec] = []
         for li, layer in enumerate((resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4)):
             for bi, blk in enumerate(layer):
@@ -209,6 +227,26 @@ class FusedStages:
         if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4:
             return False
         Nb, C, H, W = x.shape
+        return self._shape_ok(Nb, H, W)
+
+    def stem_supported(self, img: torch.Tensor) -> bool:
+        """The image batch can enter at the stem: a stem conv without max-pool, an input that
+        needs no gradient, and stem-output rows per view that tile (256-row BatchNorm-backward
+        prologue splits of the stem weight gradient)."""
+        if not (getattr(self, "stem_fused", False) and self.stem is not None):
+            return False
+        if (img.requires_grad or img.dtype != torch.bfloat16 or not img.is_cuda
+                or img.dim() != 4 or img.shape[1] % 8 or img.shape[1] < self.stem.conv.in_channels):
+            return False
+        Nb, _, H, W = img.shape
+        cs = self.stem
+        OH = (H + 2 * cs.pad - cs.k) // cs.stride + 1
+        OW = (W + 2 * cs.pad - cs.k) // cs.stride + 1
+        if Nb % self.S or ((Nb // self.S) * OH * OW) % 256:
+            return False
+        return self._shape_ok(Nb, OH, OW)
+
+    def _shape_ok(self, Nb: int, H: int, W: int) -> bool:
         if Nb % self.S or H != W:
             return False
         n = Nb // self.S
@@ -380,8 +418,10 @@ class FusedStages:
             if _SKIP_WGRAD:  # attribution experiment only: the step without weight gradients
                 _deliver_grad(cs.conv.weight, lambda out: None)
                 return
+            # creal: the stem's 3 image channels are gathered as 8 (zero-padded)
             _deliver_grad(cs.conv.weight,
-                          lambda out: run_wgrad(ops, dyn, xn, out, g, C, pro=pro, dpro=dpro))
+                          lambda out: run_wgrad(ops, dyn, xn, out, g, cs.conv.in_channels,
+                                                pro=pro, dpro=dpro))
 
         side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
         if side is None:
@@ -764,6 +804,25 @@ class FusedStages:
         _ext.TAG = ""
         return x, tapes
 
+    def stem_forward(self, img: torch.Tensor):
+        """Stem conv (statistics epilogue) → BatchNorm finalize → BN + ReLU apply with the
+        ReLU bitmask (the stem is the producer of layer1.0 like one block of another), then the
+        blocks.  Returns (output, tapes, stem tape)."""
+        ops = _ext.ops()
+        st = pstate.get()
+        S = self.S
+        cs = self.stem
+        _ext.TAG = "stem fwd"
+        a, partial, nblk = self._conv_fwd(ops, img, cs, None, S)
+        rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
+        bs = self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st)
+        x0 = torch.empty_like(a)
+        mask = torch.empty((a.numel() // 8,), device=a.device, dtype=torch.uint8)
+        ops.bn_apply_ss(a, bs.ss, None, None, x0, S, True, mask)
+        tp = _BlockTape(x=img, acts=[a], bns=[bs], out=x0, mask=mask)
+        out, tapes = self.forward(x0)
+        return out, tapes, tp
+
     def _out_apply(self, ops, pend, S: int) -> None:
         """Block output = relu(bn3(aL) + shortcut) and its ReLU bitmask, as its own pass."""
         aL, ss, res, rss, out, mask = pend
@@ -783,7 +842,10 @@ class FusedStages:
         rows_seg = ad.shape[0] * ad.shape[1] * ad.shape[2] // S
         tp.bnd = self._bn_fwd(ops, b.down.bn, partial, nblk, rows_seg, S, st, slot=slot)
 
-    def backward(self, gout: torch.Tensor, tapes: List[_BlockTape]) -> torch.Tensor:
+    def backward(self, gout: torch.Tensor, tapes: List[_BlockTape],
+                 stem_tape: Optional[_BlockTape] = None) -> Optional[torch.Tensor]:
+        """Gradient w.r.t. the executor input, or None with ``stem_tape`` (the stem's
+        parameter gradients are delivered and the image needs none)."""
         ops = _ext.ops()
         st = pstate.get()
         S = self.S
@@ -802,9 +864,20 @@ class FusedStages:
             if store is not None:
                 store.producer_streams = [main, self._side]
         g, pre = gout, None
+        stem_prev = (self._stem_block, stem_tape) if stem_tape is not None else None
         for idx in range(len(self.blocks) - 1, -1, -1):
-            prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else None
+            prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else stem_prev
             g, pre = self._block_backward(ops, st, S, self.blocks[idx], tapes[idx], g, pre, prev)
+        if stem_tape is not None:
+            # g = dL/d(stem output)·[y > 0] with the stem BatchNorm's partials from layer1.0's
+            # conv1 dgrad epilogue: finish its backward, weight gradient with the BN backward in
+            # the dY prologue (da never materialised)
+            _ext.TAG = "stem bwd"
+            coef = self._bn_bwd_finish(ops, pre[0], S)
+            _ext.TAG = "stem wgrad"
+            self._wgrad(ops, g, stem_tape.x, self.stem, None, S, bnb=(stem_tape.acts[0], coef))
+            _ext.TAG = ""
+            g = None
         if main is not None:
             if store is not None and getattr(store, "defer_side_join", False):
                 # joined in store.finish(), after the stem's backward
@@ -958,6 +1031,35 @@ class FusedStages:
             self._wgrad(ops, dad, tp.x, b.down, None, S)
         _ext.TAG = ""
         return dx, h
+
+
+class FusedStemStagesFn(torch.autograd.Function):
+    """Autograd boundary around stem + executor: input = the image batch (channels_last bf16,
+    no gradient), output = last block output; every parameter gradient bypasses autograd (flat
+    store).  ``anchor`` (the stem weight) makes autograd call the backward."""
+
+    @staticmethod
+    def forward(ctx, img, anchor, ex: FusedStages):
+        xn = img.permute(0, 2, 3, 1)
+        if not xn.is_contiguous():
+            xn = img.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+        out, tapes, stem_tape = ex.stem_forward(xn)
+        ctx.ex = ex
+        ctx.tapes = tapes
+        ctx.stem_tape = stem_tape
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gout):
+        if gout.dtype != torch.bfloat16:
+            gout = gout.to(torch.bfloat16)
+        gn = gout.permute(0, 2, 3, 1)
+        if not gn.is_contiguous():
+            gn = gout.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+        ctx.ex.backward(gn, ctx.tapes, ctx.stem_tape)
+        ctx.tapes = None
+        ctx.stem_tape = None
+        return None, None, None
 
 
 class FusedStagesFn(torch.autograd.Function):

@@ -160,7 +160,7 @@ class ResNet(nn.Module):
     # path; ``use_fused_stages = False`` (or SIMCLR_FUSED=0) keeps the per-module path
     use_fused_stages = os.environ.get("SIMCLR_FUSED", "1") != "0"
 
-    def _fused_executor(self, x: torch.Tensor, segments: int):
+    def _fused_executor(self, x: torch.Tensor, segments: int, check: bool = True):
         if not (self.training and self.use_fused_stages and torch.is_grad_enabled()
                 and x.is_cuda and x.dtype == torch.bfloat16):
             return None
@@ -172,9 +172,14 @@ class ResNet(nn.Module):
         ex = cache.get(segments)
         if ex is None:
             ex = cache[segments] = FusedStages(self, segments)
-        return ex if ex.supported(x) else None
+        return ex if (not check or ex.supported(x)) else None
 
     def forward_features(self, x: torch.Tensor, segments: int = 1) -> torch.Tensor:
+        ex = self._fused_executor(x, segments, check=False)
+        if ex is not None and ex.stem_supported(x):
+            # stem + layer1..layer4 in the executor (models/fused.py stem_forward)
+            from .fused import FusedStemStagesFn
+            return global_avg_pool(FusedStemStagesFn.apply(x, self.conv1.weight, ex))
         x = self.bn1(self.conv1(x), relu=True, segments=segments)
         x = self.maxpool(x)
         ex = self._fused_executor(x, segments)
