@@ -401,7 +401,7 @@ class FusedStages:
                                    S)
 
     def _wgrad(self, ops, dyn, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int,
-               bnb: Optional[Tuple] = None):
+               bnb: Optional[Tuple] = None, main: bool = False):
         """``bnb = (a, coef)``: dy = coef.A·dyn + coef.B·a + coef.D, the BatchNorm backward of
         the conv's own BN, computed in the dY operand's prologue (never written to HBM)."""
         Nb, H, W, C = xn.shape
@@ -424,7 +424,7 @@ class FusedStages:
                                                 pro=pro, dpro=dpro))
 
         side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
-        if side is None:
+        if side is None or main:
             run()
             return
         # operands stay referenced until the join (the caching allocator must not hand their
@@ -875,7 +875,10 @@ class FusedStages:
             _ext.TAG = "stem bwd"
             coef = self._bn_bwd_finish(ops, pre[0], S)
             _ext.TAG = "stem wgrad"
-            self._wgrad(ops, g, stem_tape.x, self.stem, None, S, bnb=(stem_tape.acts[0], coef))
+            # on the main stream: nothing else is left for it, while the weight-gradient stream
+            # still works through layer1.0's (the tail of the step runs both side by side)
+            self._wgrad(ops, g, stem_tape.x, self.stem, None, S, bnb=(stem_tape.acts[0], coef),
+                        main=True)
             _ext.TAG = ""
             g = None
         if main is not None:
