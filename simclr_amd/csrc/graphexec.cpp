@@ -8,10 +8,11 @@
 // parameters: kernel arguments, grids, memset descriptors) but issues it itself:
 //
 //   * nodes in a topological order that follows capture order (ties by creation index);
-//   * each node on one of at most `max_streams` HIP streams: a node continues the stream whose
-//     last node is one of its parents, else takes a stream whose last node is an ancestor (no
-//     false dependency), else opens a new stream, else (all streams busy with concurrent work)
-//     the stream whose tail was issued earliest;
+//   * each node on one of at most `max_streams` HIP streams: a node continues its parent's
+//     stream when it is that parent's heir (the child with the longest path to the end of the
+//     graph), else takes a stream whose last node is an ancestor and not waiting for its own
+//     heir, else opens a new stream, else (all streams busy with concurrent work) the stream
+//     whose tail was issued earliest;
 //   * a cross-stream edge becomes hipEventRecord / hipStreamWaitEvent, pruned with per-stream
 //     vector clocks (a wait is issued only when the consumer's stream does not already follow
 //     the producer's event transitively);
@@ -148,6 +149,25 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
   auto is_anc = [&](int a_pos, int v_pos) {
     return (anc[(size_t)v_pos * words + a_pos / 64] >> (a_pos % 64)) & 1ull;
   };
+  // heir of every node: the child that continues its stream — the one with the longest path
+  // to the end of the graph (the critical chain, hundreds of nodes, not a weight-gradient
+  // branch of two that ends at the final join), ties by capture order.  The other children
+  // start on other streams, behind an event.  Continuing whichever child was captured first
+  // put e.g. the downsample branch on the main chain's stream and moved the chain itself
+  // behind an event (~20 µs of dependency latency at every such fork).
+  std::vector<int> blevel(n, 0), heir(n, -1);
+  for (size_t q = n; q-- > 0;) {
+    const int v = topo[q];
+    int best = 0;
+    for (int c : children[v]) {
+      const int cp = pos[c];
+      if (heir[q] < 0 || blevel[cp] > best || (blevel[cp] == best && cp < heir[q])) {
+        best = blevel[cp];
+        heir[q] = cp;
+      }
+    }
+    blevel[q] = 1 + best;
+  }
   std::vector<int> tail(K, -1);      // topo position of each stream's last node
   std::vector<int> seq(n, 0);        // position of the node within its stream (1-based)
   std::vector<int> slen(K, 0);
@@ -164,18 +184,28 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
       for (size_t w = 0; w < words; ++w) av[w] |= au[w];
       av[up / 64] |= 1ull << (up % 64);
     }
-    // stream choice
+    // stream choice: (1) the stream of a parent whose heir this node is; (2) a stream whose
+    // tail is an ancestor and is not waiting for its own heir (reserved); (3) a new stream;
+    // (4) a reserved ancestor stream; (5) the earliest tail (all streams run concurrent work)
     int s = -1;
-    for (int u : parents[v]) {  // continue a parent's stream (first parent in capture order)
+    for (int u : parents[v]) {
+      const int up = pos[u];
+      if (heir[up] != (int)p) continue;
       for (int k = 0; k < used && s < 0; ++k)
-        if (tail[k] == pos[u]) s = k;
+        if (tail[k] == up) s = k;
       if (s >= 0) break;
     }
+    auto reserved = [&](int k) {
+      return tail[k] >= 0 && heir[tail[k]] > (int)p;  // its heir comes later
+    };
+    if (s < 0)
+      for (int k = 0; k < used && s < 0; ++k)
+        if ((tail[k] < 0 || is_anc(tail[k], (int)p)) && !reserved(k)) s = k;
+    if (s < 0 && used < K) s = used++;
     if (s < 0)
       for (int k = 0; k < used && s < 0; ++k)
         if (tail[k] < 0 || is_anc(tail[k], (int)p)) s = k;
-    if (s < 0 && used < K) s = used++;
-    if (s < 0) {  // every stream runs concurrent work: the earliest tail serialises least
+    if (s < 0) {
       s = 0;
       for (int k = 1; k < used; ++k)
         if (tail[k] < tail[s]) s = k;
