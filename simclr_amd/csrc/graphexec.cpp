@@ -10,8 +10,9 @@
 //   * nodes in a topological order that follows capture order (ties by creation index);
 //   * each node on one of at most `max_streams` HIP streams: a node continues its parent's
 //     stream when it is that parent's heir (the child with the longest path to the end of the
-//     graph), else takes a stream whose last node is an ancestor and not waiting for its own
-//     heir, else opens a new stream, else (all streams busy with concurrent work) the stream
+//     graph), else takes a stream whose last node is an ancestor (but not a parent whose heir is
+//     still to come), else opens a new stream, else (all streams busy with concurrent work) the
+//     stream
 //     whose tail was issued earliest;
 //   * a cross-stream edge becomes hipEventRecord / hipStreamWaitEvent, pruned with per-stream
 //     vector clocks (a wait is issued only when the consumer's stream does not already follow
@@ -185,7 +186,7 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
       av[up / 64] |= 1ull << (up % 64);
     }
     // stream choice: (1) the stream of a parent whose heir this node is; (2) a stream whose
-    // tail is an ancestor and is not waiting for its own heir (reserved); (3) a new stream;
+    // tail is an ancestor and not a parent still waiting for its heir (reserved); (3) a new one;
     // (4) a reserved ancestor stream; (5) the earliest tail (all streams run concurrent work)
     int s = -1;
     for (int u : parents[v]) {
@@ -195,8 +196,13 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
         if (tail[k] == up) s = k;
       if (s >= 0) break;
     }
+    // a stream whose tail is a parent of this node (which is not that parent's heir: else (1)
+    // took it) is kept for the parent's heir, which comes later in capture order
     auto reserved = [&](int k) {
-      return tail[k] >= 0 && heir[tail[k]] > (int)p;  // its heir comes later
+      if (tail[k] < 0 || heir[tail[k]] <= (int)p) return false;
+      for (int u : parents[v])
+        if (pos[u] == tail[k]) return true;
+      return false;
     };
     if (s < 0)
       for (int k = 0; k < used && s < 0; ++k)
