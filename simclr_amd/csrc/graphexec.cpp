@@ -28,6 +28,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <queue>
 #include <unordered_map>
