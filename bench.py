@@ -150,6 +150,7 @@ def run_ours(args, rank, world, dev):
     ds = synthetic_dataset(n_img, 10, size=args.size, seed=rank)
     loader = ContrastiveLoader(ds, args.batch, dev, rank=rank, world=world,
                                strength=cfg["experiment"]["strength"], seed=7, views=2)
+    loader.with_labels = False
     tr = Trainer(cfg, st, 50000)
     args.dtype = tr.precision  # fp32 on a CPU rehearsal
     tr.guard.on_error = "defer"  # an IPC timeout is checked collectively below (ipc_guard)
@@ -238,6 +239,8 @@ def run_ours(args, rank, world, dev):
                                               and tr.sreplay is not None) else "graph")
     args.graph = tr.graph is not None
     args.exec_used = _exec_mode(tr)
+    if tr.graph is not None:
+        loader.out = tr._static_x  # the augmentation writes the replayed step's input in place
     loss = None
 
     def measure():

@@ -87,6 +87,10 @@ class ContrastiveLoader:
         else:
             self.images = dataset.images
         self.labels = torch.from_numpy(dataset.labels).to(self.device)
+        # pre-training ignores the labels (no per-step label gather) and may hand the loader the
+        # captured step's static input, so the augmentation writes straight into it (no copy)
+        self.with_labels = True
+        self.out: Optional[torch.Tensor] = None
 
     def set_epoch(self, epoch: int) -> None:
         self.epoch = epoch
@@ -101,8 +105,12 @@ class ContrastiveLoader:
     def batch_from_indices(self, idx: torch.Tensor, counter: int) -> torch.Tensor:
         n = idx.numel()
         if self.gpu:
-            out = torch.empty((self.views * n, CPAD, self.OH, self.OW), device=self.device,
-                              dtype=torch.bfloat16, memory_format=torch.channels_last)
+            shape = (self.views * n, CPAD, self.OH, self.OW)
+            out = self.out
+            if out is None or tuple(out.shape) != shape or not out.is_contiguous(
+                    memory_format=torch.channels_last):
+                out = torch.empty(shape, device=self.device, dtype=torch.bfloat16,
+                                  memory_format=torch.channels_last)
             torch.ops.simclr_amd.augment(self.images, idx, n, self.views, self.OH, self.OW, CPAD,
                                          self.strength, self.seed, counter, 0,
                                          1 if self.augment else 0, out.permute(0, 2, 3, 1), None)
@@ -134,7 +142,7 @@ class ContrastiveLoader:
             idx = idx_all[s * self.n:(s + 1) * self.n]
             x = self.batch_from_indices(idx, self.counter)
             self.counter += 1
-            yield x, self.labels[idx]
+            yield x, (self.labels[idx] if self.with_labels else None)
 
 
 class EvalLoader:

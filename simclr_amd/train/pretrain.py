@@ -126,7 +126,8 @@ class Trainer:
     def step(self, x: torch.Tensor) -> torch.Tensor:
         x = self.prepare(x)
         if self.graph is not None:
-            self._static_x.copy_(x)
+            if x.data_ptr() != self._static_x.data_ptr():  # (the loader may write in place)
+                self._static_x.copy_(x)
             if self.replay_mode == "streams" and self.sreplay is not None:
                 self.sreplay.replay()
             else:
@@ -211,6 +212,7 @@ def pretrain(cfg) -> dict:
     loader = ContrastiveLoader(ds, cfg["experiment"]["batches"], st.device, rank=rank,
                                world=st.world_size, strength=cfg["experiment"]["strength"],
                                seed=seed, views=2)
+    loader.with_labels = False  # SimCLR pre-training uses no labels
     tr = Trainer(cfg, st, len(ds))
     epochs = cfg["parameter"]["epochs"]
     start_epoch = 1
@@ -246,6 +248,7 @@ def pretrain(cfg) -> dict:
             if use_graph and tr.graph is None:
                 tr.capture(x)
                 tr.replay_mode = str(cfg_get(cfg, "runtime.replay", "streams"))
+                loader.out = tr._static_x  # later batches are augmented in place
             loss = tr.step(x)
             nsteps += 1
             step_global += 1
