@@ -962,6 +962,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("ipc_collective(int op, Tensor src, Tensor(a!) dst, Tensor peers, Tensor(b!) arena, int site, Tensor(c!) epoch, Tensor(d!) err, int world, int rank) -> ()", &ipc_collective_op);
   m.def("ipc_coll_blocks() -> int", []() -> int64_t { return IPC_COLL_BLOCKS; });
   m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0) -> ()", &bn_reduce_fused_op);
+  // the ticket arrays are allocated outside any capture: Trainer.capture() calls this first
+  m.def("bn_tickets_init(Tensor like) -> ()", [](const Tensor& like) { (void)tickets_for(like, 0, 0); });
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);

@@ -158,6 +158,12 @@ class Trainer:
             torch.cuda.synchronize(self.device)
             time.sleep(1.0)
         self._static_x = x.clone()
+        if self.device.type == "cuda":
+            from ..ops import _ext
+            if _ext.available():
+                # the last-arriver reductions' persistent ticket arrays cannot be allocated
+                # inside the capture (a capture with no eager warm-up step reaches them first)
+                torch.ops.simclr_amd.bn_tickets_init(self._static_x)
         g = torch.cuda.CUDAGraph(keep_graph=True)
         # with collectives in the step, the RCCL watchdog thread polls work events while the
         # capture is open: thread-local capture mode keeps those queries legal
