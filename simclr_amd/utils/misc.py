@@ -61,7 +61,8 @@ class MetricsWriter:
 
 # attribution knobs that change the math (bench / tools only): a leftover export in a training
 # shell would silently train a wrong model
-EXPERIMENT_KNOBS = ("SIMCLR_SKIP_WGRAD", "SIMCLR_EXPERIMENT_WGRAD_SLABS")
+EXPERIMENT_KNOBS = ("SIMCLR_SKIP_WGRAD", "SIMCLR_EXPERIMENT_WGRAD_SLABS",
+                    "SIMCLR_EXPERIMENT_SKIP_BNREDUCE")
 
 
 def refuse_experiment_knobs(where: str) -> None:
