@@ -7,6 +7,7 @@
 // per-thread fixed channel chunk so scale/shift live in registers, fp32 math, deterministic
 // two-level reductions (block partials, then one reduce pass) — no float atomics.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -88,10 +89,20 @@ __device__ __forceinline__ float4 l1_slice(const float* __restrict__ partial, in
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c4 < C) {
     const float* src = partial + (size_t)s * nblk * 2 * C + (j >> 4) * C + c4;
-#pragma unroll 4
-    for (int i = beg + rl; i < end; i += 8) {
-      const float4 v = *(const float4*)(src + (size_t)i * 2 * C);
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    // batches of U rows per thread, every load of a batch issued before the first is summed
+    // (rows ascending per thread, as before: the same sums bit for bit).  The plain loop was
+    // compiled as 4-deep load groups: one dependent ~µs trip per 4 rows of a cold slice
+    constexpr int U = 8;
+    for (int i0 = beg + rl; i0 < end; i0 += 8 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u] = i0 + 8 * u < end ? *(const float4*)(src + (size_t)(i0 + 8 * u) * 2 * C)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
     }
   }
   red[rl][j] = acc;
@@ -322,15 +333,12 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
   }
   __syncthreads();
   if (!last) return;
-  // consumer: ONE agent acquire (drops this CU's stale L1 lines), then every (segment, slice)
-  // row of the 64-channel group loaded at once by all 256 threads (16-byte loads, all in
-  // flight together: the slices come from other XCDs through memory, so each dependent round
-  // trip costs ~µs) and combined through LDS in a fixed order
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+  // consumer: no agent acquire — every slice was stored sc1 and drained before its block's
+  // ticket add, and the last arriver reads every one of them with sc1 loads (L1 bypass;
+  // guide §6 Guideline 16 Rule, MI355X_MICROARCH.md visibility table row 1: ticket form, the
+  // other waves behind the barrier above), which saves the acquire's ~1.7 µs.  Every (segment,
+  // slice) row of the 64-channel group is loaded at once by all 256 threads and combined
+  // through LDS in a fixed order
   }  // !direct
   {
     const int j = threadIdx.x & 31, rl = threadIdx.x >> 5;
@@ -338,20 +346,44 @@ __global__ __launch_bounds__(256) void k_bn_reduce_fused(BnReduceArgs p) {
     float4 acc[kMaxSeg];
 #pragma unroll
     for (int sg = 0; sg < kMaxSeg; ++sg) acc[sg] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c4 < C) {
-      const float* base = src2 + (j >> 4) * C + c4;
-#pragma unroll 4
-      for (int g = rl; g < G; g += 8) {
+    // one code path per load form (the cache-policy operand is an immediate): a per-load
+    // select between them was compiled load -> wait -> load, serialising the batch
+    const bool handoff = !p.direct;
+    const float* rb = handoff ? p.ws : p.partial;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)rb, (short)0, (int)((size_t)S * G * 2 * C * 4), 0x00020000);
+    auto sum_rows = [&](auto aux) {
+      constexpr int AUX = decltype(aux)::value;
+      if (c4 >= C) return;
+      const int base = (j >> 4) * C + c4;  // float offset of this thread's row-0 element
+      constexpr int U = 4;
+      for (int g0 = rl; g0 < G; g0 += 8 * U) {
+        u32x4 v[kMaxSeg][U];
 #pragma unroll
-        for (int sg = 0; sg < kMaxSeg; ++sg) {
-          if (sg < S) {
-            float4* src = (float4*)(base + (((size_t)sg * G + g) * 2) * C);
-            const float4 v = *src;
-            acc[sg].x += v.x; acc[sg].y += v.y; acc[sg].z += v.z; acc[sg].w += v.w;
+        for (int u = 0; u < U; ++u) {
+          const int g = g0 + 8 * u;
+#pragma unroll
+          for (int sg = 0; sg < kMaxSeg; ++sg) {
+            const bool ok = sg < S && g < G;
+            // out-of-range rows read an offset past the resource: the buffer load returns 0
+            const int off = ok ? (int)(((size_t)(sg * G + g) * 2 * C + base) * 4) : 0x7fffffff;
+            v[sg][u] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, AUX);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int sg = 0; sg < kMaxSeg; ++sg) {
+            acc[sg].x += __uint_as_float(v[sg][u][0]); acc[sg].y += __uint_as_float(v[sg][u][1]);
+            acc[sg].z += __uint_as_float(v[sg][u][2]); acc[sg].w += __uint_as_float(v[sg][u][3]);
           }
         }
       }
-    }
+    };
+    if (handoff)
+      sum_rows(std::integral_constant<int, 16>{});  // sc1
+    else
+      sum_rows(std::integral_constant<int, 0>{});
 #pragma unroll
     for (int sg = 0; sg < kMaxSeg; ++sg) red4[sg * 8 + rl][j] = acc[sg];  // red4: [kMaxSeg*8][32]
   }
