@@ -2,7 +2,6 @@
 // HIP stream (so they compose with hipGraph capture and side-stream overlap) and validates the
 // shapes / dtypes / devices the kernels assume before any launch (a bad shape must never reach a
 // hand-written kernel: an out-of-bounds access can take the whole node down).
-#include <array>
 #include <ATen/core/Tensor.h>
 #include <ATen/ops/empty.h>
 #include <ATen/ops/zeros.h>
@@ -98,37 +97,6 @@ ConvFusion fusion_from(const c10::optional<Tensor>& pro_sc, const c10::optional<
 
 unsigned* tickets_for(const Tensor& like, int64_t n, int64_t slot);
 
-// in-launch forward BatchNorm finalize (conv.hip fin_publish / fin_tail): persistent zeroed
-// arenas of tagged words per device and stream slot (the readers reset every word they consume,
-// so an arena is clean between launches) and the launch plan (chunk size, chunks per XCD range)
-constexpr int64_t kFinL1Words = (int64_t)1 << 21;  // 16 MiB: [tiles][2][BN]
-constexpr int64_t kFinL2Words = (int64_t)1 << 18;  //  2 MiB: [nNb][S][8][maxc][2][BN]
-constexpr int kFinGrp = 64;
-struct FinArena {
-  Tensor l1, l2, err;
-};
-FinArena& fin_arena_for(const Tensor& like, int64_t slot);
-struct FinPlan {
-  bool ok = false;
-  int nNb = 0, grp = 0, maxc = 0;
-};
-FinPlan fin_plan(int variant, const ConvGeom& g, int S) {
-  FinPlan pl;
-  if (!igemm_fin_ok(variant, g, S)) return pl;
-  const int BM = igemm_variant_bm(variant), BN = igemm_variant_bn(variant);
-  const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
-  const int64_t nMb = M / BM, nNb = (g.N + BN - 1) / BN, nwg = nMb * nNb;
-  const int64_t nbs = nMb / S;
-  const int64_t per_x = (nwg / 8 + 1 + nNb - 1) / nNb;  // column tiles in one XCD range
-  const int64_t per_xs = std::min(per_x, nbs);
-  pl.nNb = (int)nNb;
-  pl.grp = kFinGrp;
-  pl.maxc = (int)((per_xs + kFinGrp - 1) / kFinGrp);
-  const int64_t l1 = nwg * 2 * BN, l2 = nNb * S * 8 * pl.maxc * 2 * BN;
-  pl.ok = nwg < ((int64_t)1 << 30) && nNb <= 4096 && l1 <= kFinL1Words && l2 <= kFinL2Words;
-  return pl;
-}
-
 
 void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optional<Tensor>& bias,
            const c10::optional<Tensor>& stats, std::vector<int64_t> gv,
@@ -142,12 +110,7 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
            const c10::optional<Tensor>& epi_mi2, const c10::optional<Tensor>& stats2,
            const c10::optional<Tensor>& pro_d, const c10::optional<Tensor>& A2,
            const c10::optional<Tensor>& pro_rss, const c10::optional<Tensor>& pro_out,
-           const c10::optional<Tensor>& pro_mask, const c10::optional<Tensor>& fin_mi,
-           const c10::optional<Tensor>& fin_ss, const c10::optional<Tensor>& fin_rm,
-           const c10::optional<Tensor>& fin_rv, const c10::optional<Tensor>& fin_nbt,
-           const c10::optional<Tensor>& fin_gamma, const c10::optional<Tensor>& fin_beta,
-           double fin_count, double fin_eps, double fin_momentum, int64_t fin_S,
-           int64_t fin_slot) {
+           const c10::optional<Tensor>& pro_mask) {
   const ConvGeom g = geom_from(gv);
   // bit 8 of epi_mode: epi_a is the stride-2 subsampled residual (conv.hip epi_load_batch)
   const bool epi_sub = (epi_mode & 256) != 0;
@@ -288,42 +251,6 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
       f.pro_rsc = f32(*pro_rss, "pro_rss");
       f.pro_rsh = f.pro_rsc + nseg * g.C;
     }
-  }
-  if (fin_mi.has_value() && fin_mi->defined()) {
-    TORCH_CHECK(epi_mode == 0 && !has_stats && stats_seg_blocks == 0 &&
-                    !(pro_d.has_value() && pro_d->defined()),
-                "igemm in-launch BN finalize: epilogue mode 0 without stats partials, no "
-                "BN-backward prologue");
-    TORCH_CHECK(fin_slot >= 0 && fin_slot < 2, "igemm in-launch BN finalize: slot 0 or 1");
-    const FinPlan pl = fin_plan((int)variant, g, (int)fin_S);
-    TORCH_CHECK(pl.ok, "igemm in-launch BN finalize: unsupported variant / shape (igemm_fin_ok)");
-    TORCH_CHECK(fin_mi->numel() >= 2 * fin_S * g.N, "igemm fin: mean/invstd must be [2][S][N]");
-    if (fin_ss.has_value() && fin_ss->defined())
-      TORCH_CHECK(fin_ss->numel() >= 2 * fin_S * g.N, "igemm fin: scale/shift must be [2][S][N]");
-    for (const auto* t : {&fin_rm, &fin_rv, &fin_gamma, &fin_beta})
-      if (t->has_value() && (*t)->defined())
-        TORCH_CHECK((*t)->numel() == g.N, "igemm fin: per-channel tensors must have N elements");
-    FinArena& ar = fin_arena_for(out, fin_slot);
-    f.fin_l1 = reinterpret_cast<uint64_t*>(ar.l1.data_ptr<int64_t>());
-    f.fin_l2 = reinterpret_cast<uint64_t*>(ar.l2.data_ptr<int64_t>());
-    f.fin_err = ar.err.data_ptr<int>();
-    f.fin_tk = tickets_for(out, pl.nNb, 2 + fin_slot);
-    f.fin_S = (int)fin_S;
-    f.fin_grp = pl.grp;
-    f.fin_maxc = pl.maxc;
-    f.fin_count = (float)fin_count;
-    f.fin_eps = (float)fin_eps;
-    f.fin_mom = (float)fin_momentum;
-    f.fin_mi = f32w(*fin_mi, "fin_mi");
-    f.fin_ss = optf32w(fin_ss, "fin_ss");
-    f.fin_rm = optf32w(fin_rm, "fin_rm");
-    f.fin_rv = optf32w(fin_rv, "fin_rv");
-    if (fin_nbt.has_value() && fin_nbt->defined()) {
-      check_dev(*fin_nbt, at::kLong, "fin_nbt");
-      f.fin_nbt = fin_nbt->data_ptr<int64_t>();
-    }
-    f.fin_gamma = optf32(fin_gamma, "fin_gamma");
-    f.fin_beta = optf32(fin_beta, "fin_beta");
   }
   conv_igemm_nt(g, bf(A, "A"), (size_t)A.numel(), bf(B, "B"), bfw(out, "out"), optf32(bias, "bias"),
                 optf32w(stats, "stats"), f, (int)variant, cur_stream());
@@ -569,25 +496,6 @@ unsigned* tickets_for(const Tensor& like, int64_t n, int64_t slot) {
     per_dev[d] = at::zeros({kTicketSlots * kTicketStride}, like.options().dtype(at::kInt));
   }
   return reinterpret_cast<unsigned*>(per_dev[d].data_ptr<int>()) + slot * kTicketStride;
-}
-
-FinArena& fin_arena_for(const Tensor& like, int64_t slot) {
-  static std::vector<std::array<FinArena, 2>> per_dev;
-  TORCH_CHECK(slot >= 0 && slot < 2, "fin arena slot out of range");
-  const int d = like.get_device();
-  if ((int)per_dev.size() <= d) per_dev.resize(d + 1);
-  FinArena& ar = per_dev[d][slot];
-  if (!ar.l1.defined()) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(cur_stream(), &cs);
-    TORCH_CHECK(cs == hipStreamCaptureStatusNone,
-                "BN finalize arenas must be allocated before graph capture (bn_tickets_init)");
-    const auto o = like.options().dtype(at::kLong);
-    ar.l1 = at::zeros({kFinL1Words}, o);
-    ar.l2 = at::zeros({kFinL2Words}, o);
-    ar.err = at::zeros({1}, like.options().dtype(at::kInt));
-  }
-  return ar;
 }
 
 void bn_reduce_fused_op(const Tensor& partial, int64_t nblk, int64_t S, int64_t C, int64_t mode,
@@ -1027,17 +935,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
   m.def("ce_topk(Tensor logits, Tensor y, float gscale, Tensor(a!) loss, Tensor(b!) rank, Tensor(c!)? dlogits=None) -> ()", &ce_topk_op);
   m.def("class_sums(Tensor X, Tensor y, int NC, Tensor(a!) sums, Tensor(b!) counts) -> ()", &class_sums_op);
-  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None, Tensor(f!)? fin_mi=None, Tensor(g!)? fin_ss=None, Tensor(h!)? fin_rm=None, Tensor(i!)? fin_rv=None, Tensor(j!)? fin_nbt=None, Tensor? fin_gamma=None, Tensor? fin_beta=None, float fin_count=0.0, float fin_eps=1e-5, float fin_momentum=0.1, int fin_S=0, int fin_slot=0) -> ()", &igemm);
-  m.def("igemm_fin_ok(int v, int[] geom, int S) -> bool", [](int64_t v, std::vector<int64_t> gv, int64_t S) {
-    return fin_plan((int)v, geom_from(gv), (int)S).ok;
-  });
-  // error word of the in-launch finalize's bounded polls (0: never timed out); read + reset
-  m.def("igemm_fin_err(Tensor like, int slot) -> int", [](const Tensor& like, int64_t slot) -> int64_t {
-    FinArena& ar = fin_arena_for(like, slot);
-    const int64_t v = ar.err.item<int>();
-    ar.err.zero_();
-    return v;
-  });
+  m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm);
   m.def("igemm_dual_ok(int v, int[] geom) -> bool", &igemm_dok);
   m.def("igemm_bm(int N) -> int", &igemm_bm);
   m.def("igemm_nvariants() -> int", &igemm_nvariants);
@@ -1065,11 +963,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("ipc_coll_blocks() -> int", []() -> int64_t { return IPC_COLL_BLOCKS; });
   m.def("bn_reduce_fused(Tensor partial, int nblk, int S, int C, int mode, Tensor(a!)? stats=None, float count=1.0, float eps=1e-5, float momentum=0.1, Tensor(b!)? rm=None, Tensor(c!)? rv=None, Tensor(d!)? mi=None, Tensor(e!)? nbt=None, Tensor? gamma=None, Tensor? beta=None, Tensor(f!)? ss=None, Tensor(g!)? dgamma=None, Tensor(h!)? dbeta=None, Tensor(i!)? coef=None, int ticket_slot=0, Tensor? ipc_peers=None, Tensor(j!)? ipc_arena=None, int ipc_site=0, Tensor(k!)? ipc_epoch=None, Tensor(l!)? ipc_err=None, int world=1, int rank=0) -> ()", &bn_reduce_fused_op);
   // the ticket arrays are allocated outside any capture: Trainer.capture() calls this first
-  m.def("bn_tickets_init(Tensor like) -> ()", [](const Tensor& like) {
-    (void)tickets_for(like, 0, 0);
-    (void)fin_arena_for(like, 0);
-    (void)fin_arena_for(like, 1);
-  });
+  m.def("bn_tickets_init(Tensor like) -> ()", [](const Tensor& like) { (void)tickets_for(like, 0, 0); });
   m.def("bn_apply_ss(Tensor x, Tensor ss, Tensor? res, Tensor? rss, Tensor(a!) y, int S, bool relu, Tensor(b!)? mask=None) -> ()", &bn_apply_ss_op);
   m.def("bn_apply(Tensor x, Tensor? res, Tensor(a!) y, Tensor mi, Tensor? gamma, Tensor? beta, int S, bool relu) -> ()", &bn_apply_op);
   m.def("bn_apply_eval(Tensor x, Tensor? res, Tensor(a!) y, Tensor rm, Tensor rv, Tensor? gamma, Tensor? beta, float eps, bool relu) -> ()", &bn_apply_eval_op);

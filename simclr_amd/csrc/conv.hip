@@ -83,21 +83,6 @@ struct IgemmArgs {
   // stats row remap (segment-major partials when one BN's rows span several launches):
   //   blk = seg * stats_seg_blocks + stats_base + (m0 - seg * seg_rows) / BM, seg = m0 / seg_rows
   int seg_rows, stats_seg_blocks, stats_base;
-  // in-launch BatchNorm finalize (EPI 0, fin_l1 != nullptr; see fin_publish / fin_tail): tagged
-  // per-tile statistics words, per-chunk words, per-column tickets, the forward finalize outputs
-  uint64_t* fin_l1;
-  uint64_t* fin_l2;
-  unsigned* fin_tk;
-  int* fin_err;
-  int fin_S, fin_nbs, fin_grp, fin_maxc;
-  float fin_count, fin_eps, fin_mom;
-  float* fin_mi;
-  float* fin_ss;
-  float* fin_rm;
-  float* fin_rv;
-  int64_t* fin_nbt;
-  const float* fin_gamma;
-  const float* fin_beta;
 };
 
 __device__ __forceinline__ u32x4 affine_relu8(u32x4 v, const float* sc, const float* sh, bool ok,
@@ -234,280 +219,6 @@ __device__ __forceinline__ void epi_load_batch(const IgemmArgs& p, int m0, int n
 template <int EPI>
 constexpr bool epi_prefetch() { return EPI == 3 || EPI == 4 || EPI == 5; }
 
-// ------------------------------------------------- in-launch BatchNorm finalize (forward, EPI 6)
-// Epilogue mode 6 = mode 0 (plain store) + this; its own instantiations, so the plain kernels
-// keep their register budgets.  Replaces the separate reduce/finalize launch after a forward
-// conv (bn.hip k_bn_reduce_fused mode 1) for single-process training.  No tile waits on another: every tile publishes its
-// per-channel Σy, Σy² as TAGGED 8-byte words {value bits, tag 1} with write-through (sc1)
-// stores and no fence / drain / atomic (MI355X_MICROARCH.md §visibility, granule hand-off).
-// Level 1: the tiles of one column nb, one XCD's lbid range (xcd_remap hands XCD x a contiguous
-// range, dispatched in lbid order) and one segment s form chunks of fin_grp consecutive tiles;
-// the chunk's LAST tile (dispatched last, so every tile it reads is resident or done) sums the
-// chunk's words, polling each until its tag is set (bounded: fin_err), writes them back as 0 (the
-// arena is clean again for the next launch) and publishes one tagged word per value.  It then
-// adds its tile count to the column's ticket; the chunk tile that completes the column (nMb
-// tiles) is level 2: it sums every chunk of the column, all segments, in a fixed order and
-// finalizes (mean / invstd, scale / shift, running statistics in segment order, as mode 1).
-// Deterministic: every sum has a fixed order independent of timing.
-constexpr int kFinMaxSeg = 4;
-constexpr long long kFinSpin = 20000000LL;  // 200 ms of the 100 MHz constant clock
-
-__host__ __device__ constexpr size_t fin_cst_bytes(int BM, int BN) {
-  return ((size_t)BM * (BN + 8) * 2 + 15) / 16 * 16;
-}
-// LDS beyond the epilogue's C image: the statistics cross-wave table [NWV][BN][2], the part
-// combine / level-2 result table, the winner flag
-__host__ __device__ constexpr int fin_cmb_floats(int BN, int NT, int S) {
-  return NT > S * 2 * BN ? NT : S * 2 * BN;
-}
-__host__ __device__ constexpr size_t fin_lds_bytes(int BM, int BN, int NT, int S) {
-  return fin_cst_bytes(BM, BN) + 4 * ((size_t)(NT / 64) * BN * 2 + fin_cmb_floats(BN, NT, S) + 4);
-}
-
-__device__ __forceinline__ int fin_xcd_of(int lbid, int nwg) {
-  const int q = nwg / 8, r = nwg % 8;
-  return lbid < r * (q + 1) ? lbid / (q + 1) : r + (lbid - r * (q + 1)) / q;
-}
-// mb range [a, b] of the column-nb tiles of segment s in XCD x's lbid range (empty: a > b)
-__device__ __forceinline__ void fin_range(int x, int nb, int s, int nwg, int nNb, int nbs,
-                                          int& a, int& b) {
-  const int q = nwg / 8, r = nwg % 8;
-  const int b0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  const int b1 = b0 + (x < r ? q + 1 : q);
-  a = b0 <= nb ? 0 : (b0 - nb + nNb - 1) / nNb;
-  b = b1 - 1 < nb ? -1 : (b1 - 1 - nb) / nNb;
-  a = max(a, s * nbs);
-  b = min(b, (s + 1) * nbs - 1);
-}
-
-// Σ of n tagged words addr(0..n-1) in index order; kFinBatch loads in flight per round (two
-// VGPRs each: 16 keeps the mode-6 kernels near their mode-0 register budgets); each word is
-// reset to 0 after it is read
-constexpr int kFinBatch = 16;
-template <class Addr>
-__device__ __forceinline__ float fin_ll_sum(int n, Addr addr, int* err, bool& dead) {
-  float acc = 0.f;
-  for (int i0 = 0; i0 < n; i0 += kFinBatch) {
-    uint64_t w[kFinBatch];
-#pragma unroll
-    for (int u = 0; u < kFinBatch; ++u)
-      w[u] = i0 + u < n ? __hip_atomic_load(addr(i0 + u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : (1ull << 32);
-    const long long t0 = (long long)wall_clock64();
-    while (true) {
-      bool pending = false;
-#pragma unroll
-      for (int u = 0; u < kFinBatch; ++u)
-        if ((uint32_t)(w[u] >> 32) != 1u) {
-          pending = true;
-          w[u] = __hip_atomic_load(addr(i0 + u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      if (!pending) break;
-      if (dead || (long long)wall_clock64() - t0 > kFinSpin) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        dead = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int u = 0; u < kFinBatch; ++u)
-      if (i0 + u < n) {
-        acc += __uint_as_float((uint32_t)w[u]);
-        __hip_atomic_store(addr(i0 + u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-  }
-  return acc;
-}
-
-__device__ __forceinline__ void fin_put(uint64_t* w, float v) {
-  __hip_atomic_store(w, (1ull << 32) | (uint64_t)__float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// statistics of the staged tile (the bf16-rounded values the store loop writes), published as
-// this tile's tagged words [lbid][2][BN]; runs before the store loop, so no store is drained
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void fin_publish(const IgemmArgs& p, char* smem, int m0, int n0,
-                                            int mb) {
-  constexpr int CST = BN + 8, CPR = BN / 8, RSTEP = NT / CPR, NIT = BM / RSTEP, NWV = NT / 64;
-  const uint16_t* Cs = (const uint16_t*)smem;
-  float* red = (float*)(smem + fin_cst_bytes(BM, BN));
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int ch = tid % CPR, r0 = tid / CPR, n = n0 + ch * 8;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-#pragma unroll 4
-  for (int it = 0; it < NIT; ++it) {
-    const int row = r0 + it * RSTEP;
-    if (m0 + row < p.M && n < p.N) {
-      const u32x4 v = *(const u32x4*)(Cs + row * CST + ch * 8);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = lo_bf(v[e]), b = hi_bf(v[e]);
-        s1[2 * e] += a; s2[2 * e] += a * a;
-        s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
-      }
-    }
-  }
-#pragma unroll
-  for (int off = CPR; off < 64; off <<= 1) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] += __shfl_xor(s1[e], off, 64);
-      s2[e] += __shfl_xor(s2[e], off, 64);
-    }
-  }
-  if (lane < CPR) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(wid * BN + ch * 8 + e) * 2 + 0] = s1[e];
-      red[(wid * BN + ch * 8 + e) * 2 + 1] = s2[e];
-    }
-  }
-  __syncthreads();
-  if (tid < BN && n0 + tid < p.N) {
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int r = 0; r < NWV; ++r) {
-      a += red[(r * BN + tid) * 2 + 0];
-      b += red[(r * BN + tid) * 2 + 1];
-    }
-    uint64_t* w = p.fin_l1 + ((size_t)(mb * p.nNb + n0 / BN) * 2) * BN + tid;
-    fin_put(w, a);
-    fin_put(w + BN, b);
-  }
-}
-
-// after the store loop: level 1 on a chunk's last tile, level 2 + finalize on a column's last
-// chunk (block-uniform control flow throughout)
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void fin_tail(const IgemmArgs& p, char* smem, int mb, int n0) {
-  const int nNb = p.nNb, nb = n0 / BN, nwg = p.nMb * nNb, nbs = p.fin_nbs, G = p.fin_grp;
-  const int S = p.fin_S;
-  const int x = fin_xcd_of(mb * nNb + nb, nwg);
-  const int s = mb / nbs;
-  int a, b;
-  fin_range(x, nb, s, nwg, nNb, nbs, a, b);
-  const int c = (mb - a) / G;
-  const int ca = a + c * G, ce = min(b, ca + G - 1);
-  if (mb != ce) return;
-  const int T = ce - ca + 1;
-  constexpr int NWV = NT / 64;
-  float* cmb = (float*)(smem + fin_cst_bytes(BM, BN)) + NWV * BN * 2;
-  int* flag = (int*)(cmb + fin_cmb_floats(BN, NT, S));
-  const int tid = threadIdx.x;
-  bool dead = false;
-  constexpr int V = 2 * BN;
-  const size_t tstride = (size_t)nNb * 2 * BN;  // words between consecutive tiles of a column
-  uint64_t* l1 = p.fin_l1 + ((size_t)(ca * nNb + nb) * 2) * BN;
-  uint64_t* l2 = p.fin_l2 + ((size_t)(((nb * S + s) * 8 + x) * p.fin_maxc + c) * 2) * BN;
-  if (c >= p.fin_maxc) {  // host sizing guarantees this never happens
-    if (tid == 0) __hip_atomic_store(p.fin_err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (V >= NT) {
-    for (int v = tid; v < V; v += NT) {
-      const int cc = v % BN;
-      if (n0 + cc >= p.N) continue;
-      uint64_t* base = l1 + v;
-      const float r = fin_ll_sum(T, [&](int i) { return base + i * tstride; }, p.fin_err, dead);
-      fin_put(l2 + v, r);
-    }
-  } else {
-    constexpr int P = V < NT ? NT / V : 1;
-    const int v = tid % V, j = tid / V, cc = v % BN;
-    float r = 0.f;
-    if (n0 + cc < p.N) {
-      uint64_t* base = l1 + v + j * tstride;
-      r = fin_ll_sum((T - j + P - 1) / P, [&](int i) { return base + (size_t)i * P * tstride; },
-                     p.fin_err, dead);
-    }
-    cmb[j * V + v] = r;
-    __syncthreads();
-    if (j == 0 && n0 + cc < p.N) {
-      float t = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < P; ++jj) t += cmb[jj * V + v];
-      fin_put(l2 + v, t);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned old =
-        __hip_atomic_fetch_add(&p.fin_tk[nb], (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int win = old + (unsigned)T == (unsigned)p.nMb;
-    if (win) __hip_atomic_store(&p.fin_tk[nb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = win;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  // ---- level 2: every chunk of column nb, segment by segment, XCD by XCD, chunk by chunk
-  const int V2 = S * V;
-  auto level2 = [&](int vv, int j, int P2) -> float {
-    const int s2 = vv / V, v = vv % V, cc = v % BN;
-    if (n0 + cc >= p.N) return 0.f;
-    int pre[9];
-    pre[0] = 0;
-#pragma unroll
-    for (int xx = 0; xx < 8; ++xx) {
-      int a2, b2;
-      fin_range(xx, nb, s2, nwg, nNb, nbs, a2, b2);
-      pre[xx + 1] = pre[xx] + (a2 <= b2 ? (b2 - a2) / G + 1 : 0);
-    }
-    const int maxc = p.fin_maxc;
-    uint64_t* base = p.fin_l2 + ((size_t)((nb * S + s2) * 8) * maxc * 2) * BN + v;
-    auto addr = [&](int i) {
-      const int t = j + i * P2;
-      int xx = 0, px = 0;
-#pragma unroll
-      for (int k = 1; k < 8; ++k)
-        if (t >= pre[k]) { xx = k; px = pre[k]; }
-      return base + ((size_t)(xx * maxc + (t - px)) * 2) * BN;
-    };
-    return fin_ll_sum((pre[8] - j + P2 - 1) / P2, addr, p.fin_err, dead);
-  };
-  if (V2 < NT) {
-    const int P2 = NT / V2;
-    const int j = tid / V2, vv = tid % V2;
-    if (j < P2) cmb[j * V2 + vv] = level2(vv, j, P2);
-    __syncthreads();
-    if (tid < V2) {
-      float t = 0.f;
-      for (int jj = 0; jj < P2; ++jj) t += cmb[jj * V2 + tid];
-      cmb[tid] = t;  // only this thread touches column tid of the part table
-    }
-  } else {
-    for (int vv = tid; vv < V2; vv += NT) cmb[vv] = level2(vv, 0, 1);
-  }
-  __syncthreads();
-  if (tid < BN && n0 + tid < p.N) {
-    const int C = p.N, ch = n0 + tid;
-    float rm = p.fin_rm ? p.fin_rm[ch] : 0.f;
-    float rv = p.fin_rv ? p.fin_rv[ch] : 0.f;
-    const float unbias = p.fin_count > 1.f ? p.fin_count / (p.fin_count - 1.f) : 1.f;
-    for (int sg = 0; sg < S; ++sg) {
-      const float mean = cmb[sg * V + tid] / p.fin_count;
-      float var = cmb[sg * V + BN + tid] / p.fin_count - mean * mean;
-      var = var > 0.f ? var : 0.f;
-      const float inv = rsqrtf(var + p.fin_eps);
-      p.fin_mi[sg * C + ch] = mean;
-      p.fin_mi[S * C + sg * C + ch] = inv;
-      if (p.fin_ss != nullptr) {
-        const float sc = (p.fin_gamma ? p.fin_gamma[ch] : 1.f) * inv;
-        p.fin_ss[sg * C + ch] = sc;
-        p.fin_ss[S * C + sg * C + ch] = (p.fin_beta ? p.fin_beta[ch] : 0.f) - mean * sc;
-      }
-      rm = (1.f - p.fin_mom) * rm + p.fin_mom * mean;
-      rv = (1.f - p.fin_mom) * rv + p.fin_mom * var * unbias;
-    }
-    if (p.fin_rm) p.fin_rm[ch] = rm;
-    if (p.fin_rv) p.fin_rv[ch] = rv;
-    if (nb == 0 && tid == 0 && p.fin_nbt != nullptr) p.fin_nbt[0] += S;
-  }
-}
-
 template <int BM, int BN, int WM, int WN, int NT, int EPI>
 __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
                                                f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
@@ -540,7 +251,6 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
     }
   }
   __syncthreads();
-  if (EPI == 6) fin_publish<BM, BN, NT>(p, smem, m0, n0, mb);
   constexpr int CPR = BN / 8;            // 16-B chunks per row
   constexpr int RSTEP = NT / CPR;        // rows per pass
   const int ch = tid % CPR;
@@ -698,7 +408,6 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmArgs& p,
       }
     }
   }
-  if (EPI == 6) fin_tail<BM, BN, NT>(p, smem, mb, n0);
 }
 
 // PRO: 0 none, 1 BN-apply + ReLU prologue, 2 BN-backward prologue (two operands)
@@ -2722,8 +2431,6 @@ void launch_igemm_t(const IgemmArgs& a0, hipStream_t s) {
   const size_t red = (size_t)(256 / (BN / 8)) * BN * 3 * 4;
   if (cst > lds) lds = cst;
   if (red > lds) lds = red;
-  if (a.fin_l1 != nullptr && fin_lds_bytes(BM, BN, 256, a.fin_S) > lds)
-    lds = fin_lds_bytes(BM, BN, 256, a.fin_S);
   hipLaunchKernelGGL((igemm_nt<BM, BN, WM, WN, PRO, EPI>), dim3(grid), dim3(256), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
@@ -2734,11 +2441,8 @@ void launch_glds_t(const IgemmArgs& a0, hipStream_t s) {
   a.nMb = (a.M + BM - 1) / BM;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
-  size_t lds = igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? NST : 1, PRO >= 2 ? 2 : 1) +
-               (PRO ? (size_t)(PRO == 3 ? 4 : PRO == 2 ? 3 : 2) * a.C * 4 : 0);
-  // (the finalize tables sit past the C image, over the dead staging / prologue table)
-  if (a.fin_l1 != nullptr && fin_lds_bytes(BM, BN, NT, a.fin_S) > lds)
-    lds = fin_lds_bytes(BM, BN, NT, a.fin_S);
+  const size_t lds = igemm_glds_pro_offset(BM, BN, NT, a.K > 64 ? NST : 1, PRO >= 2 ? 2 : 1) +
+                     (PRO ? (size_t)(PRO == 3 ? 4 : PRO == 2 ? 3 : 2) * a.C * 4 : 0);
   hipLaunchKernelGGL((igemm_glds<BM, BN, WM, WN, PRO, EPI, NST>), dim3(a.nMb * a.nNb), dim3(NT),
                      lds, s, a);
   HIP_CHECK_LAUNCH();
@@ -2758,11 +2462,8 @@ void launch_patch_t(const IgemmArgs& a0, hipStream_t s) {
   a.nMb = (a.M + 255) / 256;
   a.nNb = (a.N + BN - 1) / BN;
   constexpr int NT = 64 * WM * WN;
-  size_t lds = igemm_patch_lds(BN, NT, a.OW, a.C);
-  if (a.fin_l1 != nullptr && fin_lds_bytes(256, BN, NT, a.fin_S) > lds)
-    lds = fin_lds_bytes(256, BN, NT, a.fin_S);
-  hipLaunchKernelGGL((igemm_patch<BN, WM, WN, EPI, PRO>), dim3(a.nMb * a.nNb), dim3(NT), lds, s,
-                     a);
+  hipLaunchKernelGGL((igemm_patch<BN, WM, WN, EPI, PRO>), dim3(a.nMb * a.nNb), dim3(NT),
+                     igemm_patch_lds(BN, NT, a.OW, a.C), s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -2779,12 +2480,7 @@ void launch_patch(const IgemmArgs& a, hipStream_t s) {
         else
           launch_patch_t<BN, WM, WN, 4, 1>(a, s);
         break;
-      default:
-        if (a.fin_l1 != nullptr)
-          launch_patch_t<BN, WM, WN, 6, 1>(a, s);
-        else
-          launch_patch_t<BN, WM, WN, 0, 1>(a, s);
-        break;
+      default: launch_patch_t<BN, WM, WN, 0, 1>(a, s); break;
     }
     return;
   }
@@ -2798,12 +2494,7 @@ void launch_patch(const IgemmArgs& a, hipStream_t s) {
       else
         launch_patch_t<BN, WM, WN, 4>(a, s);
       break;
-    default:
-      if (a.fin_l1 != nullptr)
-        launch_patch_t<BN, WM, WN, 6>(a, s);
-      else
-        launch_patch_t<BN, WM, WN, 0>(a, s);
-      break;
+    default: launch_patch_t<BN, WM, WN, 0>(a, s); break;
   }
 }
 
@@ -2836,10 +2527,7 @@ void launch_glds(const IgemmArgs& a, hipStream_t s) {
   }
   if (a.pro_out != nullptr) {  // block-output prologue: 2 stages, plain epilogue (host-checked)
     if constexpr (NST == 2) {
-      if (a.fin_l1 != nullptr)
-        launch_glds_t<BM, BN, WM, WN, 3, 6, NST>(a, s);
-      else
-        launch_glds_t<BM, BN, WM, WN, 3, 0, NST>(a, s);
+      launch_glds_t<BM, BN, WM, WN, 3, 0, NST>(a, s);
     } else {
       fprintf(stderr, "igemm: 3-stage LDS-DMA variant with the block-output prologue\n");
       abort();
@@ -2852,12 +2540,7 @@ void launch_glds(const IgemmArgs& a, hipStream_t s) {
         case 1: launch_glds_t<BM, BN, WM, WN, 1, 1, NST>(a, s); break;
         case 2: launch_glds_t<BM, BN, WM, WN, 1, 2, NST>(a, s); break;
         case 3: launch_glds_t<BM, BN, WM, WN, 1, 3, NST>(a, s); break;
-        default:
-          if (a.fin_l1 != nullptr)
-            launch_glds_t<BM, BN, WM, WN, 1, 6, NST>(a, s);
-          else
-            launch_glds_t<BM, BN, WM, WN, 1, 0, NST>(a, s);
-          break;
+        default: launch_glds_t<BM, BN, WM, WN, 1, 0, NST>(a, s); break;
       }
     } else {
       fprintf(stderr, "igemm: 3-stage LDS-DMA variant with a prologue\n");
@@ -2875,12 +2558,7 @@ void launch_glds(const IgemmArgs& a, hipStream_t s) {
       else
         launch_glds_t<BM, BN, WM, WN, 0, 4, NST>(a, s);
       break;
-    default:
-      if (a.fin_l1 != nullptr)
-        launch_glds_t<BM, BN, WM, WN, 0, 6, NST>(a, s);
-      else
-        launch_glds_t<BM, BN, WM, WN, 0, 0, NST>(a, s);
-      break;
+    default: launch_glds_t<BM, BN, WM, WN, 0, 0, NST>(a, s); break;
   }
 }
 
@@ -2903,12 +2581,7 @@ void launch_igemm(const IgemmArgs& a, hipStream_t s) {
       case 1: launch_igemm_t<BM, BN, WM, WN, 1, 1>(a, s); break;
       case 2: launch_igemm_t<BM, BN, WM, WN, 1, 2>(a, s); break;
       case 3: launch_igemm_t<BM, BN, WM, WN, 1, 3>(a, s); break;
-      default:
-        if (a.fin_l1 != nullptr)
-          launch_igemm_t<BM, BN, WM, WN, 1, 6>(a, s);
-        else
-          launch_igemm_t<BM, BN, WM, WN, 1, 0>(a, s);
-        break;
+      default: launch_igemm_t<BM, BN, WM, WN, 1, 0>(a, s); break;
     }
     return;
   }
@@ -2922,12 +2595,7 @@ void launch_igemm(const IgemmArgs& a, hipStream_t s) {
       else
         launch_igemm_t<BM, BN, WM, WN, 0, 4>(a, s);
       break;
-    default:
-      if (a.fin_l1 != nullptr)
-        launch_igemm_t<BM, BN, WM, WN, 0, 6>(a, s);
-      else
-        launch_igemm_t<BM, BN, WM, WN, 0, 0>(a, s);
-      break;
+    default: launch_igemm_t<BM, BN, WM, WN, 0, 0>(a, s); break;
   }
 }
 
@@ -3310,29 +2978,6 @@ bool igemm_patch_ok(const ConvGeom& g) {
 }
 // block-output prologue (PRO 3): 2-stage LDS-DMA tiles whose doubled A staging fits the LDS,
 // on 1x1 / stride-1 / unpadded / direct-output convolutions (A row m = output row m)
-// threads of variant v's block (the launch switch in conv_igemm_nt)
-static int igemm_variant_nt(int v) {
-  static const int NT[] = {256, 256, 256, 256, 256, 256, 256,             // igemm_nt
-                           512, 512, 256, 256, 512, 512, 256, 512,        // glds 7-14
-                           256, 512,                                      // patch 15-16
-                           512, 256, 512,                                 // glds 17-19
-                           256, 256};                                     // glds 20-21
-  static_assert(sizeof(NT) / sizeof(NT[0]) == sizeof(IG_VARIANTS) / sizeof(IG_VARIANTS[0]),
-                "variant thread table");
-  return NT[v];
-}
-
-bool igemm_fin_ok(int v, const ConvGeom& g, int S) {
-  if (v < 0 || v >= igemm_num_variants() || S < 1 || S > kFinMaxSeg) return false;
-  const int BM = IG_VARIANTS[v][0], BN = IG_VARIANTS[v][1], NT = igemm_variant_nt(v);
-  const long long M = (long long)g.Nb * g.OH * g.OW;
-  if (M % S || (M / S) % BM) return false;
-  // two resident blocks per CU (single-stage LDS-DMA tiles, small register-staged tiles) must
-  // keep fitting twice
-  const bool two = v >= IG_GLDS1 || (v < IG_GLDS0 && BM * BN <= 128 * 128);
-  return fin_lds_bytes(BM, BN, NT, S) <= (two ? 80 : 160) * 1024;
-}
-
 bool igemm_dual_ok(int v, const ConvGeom& g) {
   if (!((v >= IG_GLDS0 && v < IG_GLDS3) || (v >= IG_GLDS8W && v < IG_GLDS1)) ||
       !igemm_glds_ok(g, true, false))
@@ -3390,20 +3035,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_c2 = f.epi_c2; a.epi_mi2 = f.epi_mi2; a.stats2 = f.stats2;
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
-  a.fin_l1 = f.fin_l1; a.fin_l2 = f.fin_l2; a.fin_tk = f.fin_tk; a.fin_err = f.fin_err;
-  a.fin_S = f.fin_S; a.fin_grp = f.fin_grp; a.fin_maxc = f.fin_maxc;
-  a.fin_count = f.fin_count; a.fin_eps = f.fin_eps; a.fin_mom = f.fin_mom;
-  a.fin_mi = f.fin_mi; a.fin_ss = f.fin_ss; a.fin_rm = f.fin_rm; a.fin_rv = f.fin_rv;
-  a.fin_nbt = f.fin_nbt; a.fin_gamma = f.fin_gamma; a.fin_beta = f.fin_beta;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
-  if (a.fin_l1 != nullptr) {
-    if (a.epi_mode != 0 || a.stats != nullptr || a.pro_d != nullptr ||
-        !igemm_fin_ok(variant, g, a.fin_S)) {
-      fprintf(stderr, "igemm: in-launch BN finalize: unsupported variant %d / epilogue\n", variant);
-      abort();  // the bindings reject this
-    }
-    a.fin_nbs = a.M / a.fin_S / igemm_variant_bm(variant);
-  }
   if (a.pro_out != nullptr
           ? !igemm_dual_ok(variant, g)
           : !igemm_variant_ok(variant, g, a.pro_sc != nullptr, a.pro_d != nullptr)) {

@@ -51,21 +51,6 @@ struct ConvFusion {
   int seg_rows = 0;               // rows per segment of the output (stats remap, mode 3)
   int stats_seg_blocks = 0;       // >0: segment-major stats rows (see conv.hip)
   int stats_base = 0;
-  // in-launch forward BatchNorm finalize (epilogue mode 0 without stats partials): conv.hip
-  // fin_publish / fin_tail.  Arenas / tickets are persistent per device and stream slot.
-  uint64_t* fin_l1 = nullptr;
-  uint64_t* fin_l2 = nullptr;
-  unsigned* fin_tk = nullptr;
-  int* fin_err = nullptr;
-  int fin_S = 0, fin_grp = 0, fin_maxc = 0;
-  float fin_count = 0.f, fin_eps = 0.f, fin_mom = 0.f;
-  float* fin_mi = nullptr;
-  float* fin_ss = nullptr;
-  float* fin_rm = nullptr;
-  float* fin_rv = nullptr;
-  int64_t* fin_nbt = nullptr;
-  const float* fin_gamma = nullptr;
-  const float* fin_beta = nullptr;
 };
 
 int igemm_num_variants();
@@ -78,7 +63,6 @@ bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro);
 // the bindings' checks and the Python autotuner's candidate lists)
 bool igemm_variant_is_patch(int v);
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro);
-bool igemm_fin_ok(int v, const ConvGeom& g, int S);  // in-launch BN finalize (fin_*)
 bool igemm_dual_ok(int v, const ConvGeom& g);  // block-output prologue (see igemm_glds)
 int igemm_block_m(int N);
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,

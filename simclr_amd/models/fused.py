@@ -53,11 +53,6 @@ _SKIP_WGRAD = os.environ.get("SIMCLR_SKIP_WGRAD", "0") == "1"
 # attribution experiment: SIMCLR_EXPERIMENT_SKIP_BNREDUCE=fwd|bwd|all drops the BatchNorm
 # reduce/finalize launches (garbage statistics): the upper bound of folding them into the convs
 _SKIP_BNRED = os.environ.get("SIMCLR_EXPERIMENT_SKIP_BNREDUCE", "")
-# experiment (off by default): forward BatchNorm statistics reduced and finalized inside the
-# producing conv (conv.hip fin_publish / fin_tail) instead of a separate reduce launch (single
-# process only).  Measured +1.2 ms/step on the bench (r5 optimisation log): the in-launch
-# hand-offs move ~64 KB per hop under full streaming load, which costs more than the launch
-BN_FIN = os.environ.get("SIMCLR_BN_FIN", "0") != "0"
 
 
 def _empty_nhwc(n, h, w, c, dev, dtype=torch.bfloat16):
@@ -150,7 +145,6 @@ class FusedStages:
         self.calls = 0
         # launch accounting (tests): block outputs formed in a conv1 prologue / as their own pass
         self.dual_launches = 0
-        self.fin_launches = 0  # convs whose BatchNorm was finalized in-launch (BN_FIN)
         self.out_apply_calls = 0
         # BN backward of a bottleneck's conv3 inside conv3's dgrad/wgrad operand prologues
         # (only up to 128 input channels: measured net loss or break-even above, r2 log)
@@ -276,17 +270,14 @@ class FusedStages:
     # ------------------------------------------------------------------ building blocks
     def _conv_bn_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int, st,
                      dual=None, slot: int = 0):
-        """a = conv(pro(x)) and the BatchNorm state of ``cs.bn`` over it: finalized inside the
-        conv launch where possible (``BN_FIN``), else statistics partials + ``_bn_fwd``."""
-        r = self._conv_fwd(ops, xn, cs, pro_ss, S, dual=dual, fin=(st, slot))
-        if len(r) == 2:
-            return r
-        a, partial, nblk = r
+        """a = conv(pro(x)) and the BatchNorm state of ``cs.bn`` over it (statistics partials
+        from the conv epilogue, one reduce / finalize launch)."""
+        a, partial, nblk = self._conv_fwd(ops, xn, cs, pro_ss, S, dual=dual)
         rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
         return a, self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st, slot=slot)
 
     def _conv_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int,
-                  dual=None, fin=None):
+                  dual=None):
         """a = conv(pro(x)) with BN statistics partials in the epilogue.
 
         ``dual = (aL, ss, res, rss, out, mask)``: the input is the previous block's output,
@@ -310,33 +301,10 @@ class FusedStages:
         elif pro_ss is not None:
             pro = (pro_ss[0], pro_ss[1], M // S, True)
         v = igemm_choose(ops, A, w, a, g, want_stats=True, pro=pro, seg_rows=M // S, dual=dl)
-        if fin is not None and self._fin_ok(ops, xn, v, g, S, fin[0]):
-            st, slot = fin
-            bn = cs.bn
-            dev = xn.device
-            count = float(M // S)
-            mi = torch.empty((2 * S * Co,), device=dev, dtype=torch.float32)
-            ss = torch.empty((2 * S * Co,), device=dev, dtype=torch.float32)
-            igemm_launch(ops, A, w, a, g, v, pro=pro, dual=dl,
-                         fin={"mi": mi, "ss": ss, "rm": bn.running_mean, "rv": bn.running_var,
-                              "nbt": bn.num_batches_tracked, "gamma": bn.weight.detach(),
-                              "beta": bn.bias.detach(), "count": count, "eps": bn.eps,
-                              "momentum": bn.momentum, "S": S, "slot": slot})
-            self.fin_launches += 1
-            return a, _BNState(mi, ss.view(2, S * Co), count)
         bm = ops.igemm_variant_bm(v)
         stats = torch.empty(((M // bm) * 2 * Co,), device=xn.device, dtype=torch.float32)
         igemm_launch(ops, A, w, a, g, v, stats=stats, pro=pro, dual=dl)
         return a, stats, M // bm // S
-
-    def _fin_ok(self, ops, xn, v: int, g, S: int, st) -> bool:
-        if not (BN_FIN and xn.is_cuda) or st.comm or _SKIP_BNRED in ("fwd", "all"):
-            return False
-        key = (v, tuple(g), S)
-        cache = self.__dict__.setdefault("_fin_cache", {})
-        if key not in cache:
-            cache[key] = bool(ops.igemm_fin_ok(v, g, S))
-        return cache[key]
 
     def _dual_ok(self, ops, xn, cs: _ConvSpec, S: int) -> bool:
         """Can ``cs`` (a block's conv1) form its input — the previous block's output — in its

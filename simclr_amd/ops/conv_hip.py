@@ -90,7 +90,7 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
                  seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None,
-                 bnb=None, dual=None, fin=None) -> None:
+                 bnb=None, dual=None) -> None:
     """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip);
     ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue;
     ``dual = (res, rss, out, mask)``: block-output prologue — A is a block's pre-BN conv3
@@ -109,16 +109,8 @@ def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=N
     em = epi[4] if epi is not None and len(epi) > 4 else None
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     c2, mi2, st2 = second if second is not None else (None, None, None)
-    kw = {}
-    if fin is not None:
-        # in-launch forward BatchNorm finalize (conv.hip fin_publish / fin_tail):
-        # fin = dict(mi, ss, rm, rv, nbt, gamma, beta, count, eps, momentum, S, slot)
-        kw = {"fin_mi": fin["mi"], "fin_ss": fin["ss"], "fin_rm": fin["rm"],
-              "fin_rv": fin["rv"], "fin_nbt": fin["nbt"], "fin_gamma": fin["gamma"],
-              "fin_beta": fin["beta"], "fin_count": fin["count"], "fin_eps": fin["eps"],
-              "fin_momentum": fin["momentum"], "fin_S": fin["S"], "fin_slot": fin["slot"]}
     ops.igemm(A, B, out, bias, stats, geom, psc, psh, pseg, prelu, emode, ea, eb, v, ess, emi,
-              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask, **kw)
+              seg_rows, remap[0], remap[1], ec, em, c2, mi2, st2, pd, A2, rss, pout, pmask)
 
 
 def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None):
