@@ -1108,21 +1108,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
                                           epi_prefetch<EPI>() ? &pre : nullptr);
 }
 
-// ------------------------------------------- 3x3 conv, persistent, resident weights (layer1)
-// The ResNet-50 layer1 3x3 conv (and its stride-1 dgrad): C = N = 64 at 32x32, K = 576.  The
-// per-tile kernel above runs at ~30 % MFMA utilisation: every block waits for its own patch
-// DMA, then for one weight tile per k-step (9 barriers), and only 2 blocks fit a CU.  Here ONE
-// block per CU (8 waves) keeps the whole weight matrix resident in LDS (9 x [64][64], 72 KiB,
-// loaded once) and walks a contiguous run of 256-pixel tiles with a double-buffered input patch:
-// tile t+1's patch is DMA'd while tile t computes, so a tile is 9 taps of MFMAs with no global
-// load or barrier inside them.  Consecutive tiles of a run are the next 8 rows of the same image
-// (their 2 halo rows were just fetched into the XCD's L2).  The epilogue (any mode) stages
-// through the tile's own patch buffer once its MFMAs are done.
-// LDS: weights 73,728 B + 2 patches x 44,032 B + the PRO table 1,024 B = 162,816 B.
-// Host guarantees (igemm_ppatch_ok): igemm_patch_ok geometry with C = N = 64, OW = 32.
-constexpr int PP_NINSTR = 43;                  // patch DMA instructions (8 pixels x 128 B each)
-constexpr int PP_PSZ = PP_NINSTR * 512;        // patch buffer, elements
-constexpr int PP_LDS = 9 * 64 * 64 * 2 + 2 * PP_PSZ * 2 + 1024;
 
 
 // ------------------------------------------------------------------------------------ wgrad
