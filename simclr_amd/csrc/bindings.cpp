@@ -945,6 +945,10 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_glds_ok(int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_gldsok);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
   m.def("wgrad_variant_glds(int v) -> bool", &wgrad_vglds);
+  m.def("wgrad_variant_area(int v) -> int", [](int64_t v) -> int64_t {
+    TORCH_CHECK(v >= 0 && v < wgrad_num_variants(), "wgrad variant out of range");
+    return wgrad_variant_area((int)v);
+  });
   m.def("igemm_variant_ok(int v, int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_vok);
   m.def("wgrad_variant_ok(int v, int[] geom, bool pro, bool dy_pro) -> bool", &wgrad_vok);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);

@@ -3057,6 +3057,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
 bool wgrad_variant_glds(int v) { return (v >= WG_GLDS0 && v < WG_PATCH0) || v >= WG_PIPE0; }
+int wgrad_variant_area(int v) { return WG_VARIANTS[v][0] * WG_VARIANTS[v][1]; }
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro) {
   if (v < 0 || v >= wgrad_num_variants()) return false;
   if (v == WG_PATCH0) return !dy_pro && g.N % 64 == 0 && igemm_patch_ok(g);

@@ -71,6 +71,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
 int wgrad_num_variants();
 int wgrad_default_variant(int N);
 bool wgrad_variant_glds(int v);  // LDS-DMA variant (see wgrad_variant_ok)
+int wgrad_variant_area(int v);   // output tile elements (BCO x BKK)
 bool wgrad_variant_ok(int v, const ConvGeom& g, bool pro, bool dy_pro);
 int wgrad_splits(const ConvGeom& g, int variant);
 void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t x_elems,

@@ -429,6 +429,9 @@ class FusedStages:
             pro = (pro_ss[0], pro_ss[1], M // S, True, S)
         dpro = (bnb[0], bnb[1], M // S, S) if bnb is not None else None
 
+        side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
+        concurrent = side is not None and not main
+
         def run():
             if _SKIP_WGRAD:  # attribution experiment only: the step without weight gradients
                 _deliver_grad(cs.conv.weight, lambda out: None)
@@ -436,9 +439,8 @@ class FusedStages:
             # creal: the stem's 3 image channels are gathered as 8 (zero-padded)
             _deliver_grad(cs.conv.weight,
                           lambda out: run_wgrad(ops, dyn, xn, out, g, cs.conv.in_channels,
-                                                pro=pro, dpro=dpro))
+                                                pro=pro, dpro=dpro, concurrent=concurrent))
 
-        side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
         if side is None or main:
             run()
             return

@@ -137,17 +137,26 @@ def run_igemm(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=N
 
 
 
-def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
+# weight gradients issued beside the dgrad / BatchNorm chain (the fused executor's side stream)
+# skip the 256 x 256 output tiles: the autotuner times candidates alone, where those tiles win,
+# but their 128 KB of LDS per block keeps every chain block off the CU; under the concurrent
+# step the best <= 256 x 128 tile is 0.17 ms/step faster (4 of 4 interleaved A/B rounds,
+# profiles/r5_optimization_log.md)
+CONCURRENT_MAX_TILE = 256 * 128
+
+
+def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None, concurrent: bool = False):
     """Split-M weight gradient (fp32, written to ``out`` = OHWI) with the autotuned variant.
 
     ``dpro = (dY2, coef[3][S][N], seg_rows, S)``: the dY operand is the BatchNorm backward
-    A·dY + B·dY2 + D computed on the fly (splits are aligned to the segments)."""
+    A·dY + B·dY2 + D computed on the fly (splits are aligned to the segments).
+    ``concurrent``: the kernel runs beside the critical chain (``CONCURRENT_MAX_TILE``)."""
     psc, psh, seg_rows, prelu, pS = pro if pro is not None else (None, None, 0, False, 1)
     dY2, dcoef, dseg, dS = dpro if dpro is not None else (None, None, 0, 1)
     N = geom[14]
     K = geom[6] * geom[7] * geom[3]
     M = geom[0] * geom[4] * geom[5]
-    key = ("wgrad", tuple(geom), creal, psc is not None, dpro is not None)
+    key = ("wgrad", tuple(geom), creal, psc is not None, dpro is not None, concurrent)
 
     def nsplit(v):
         splits = ops.wgrad_splits(geom, v)
@@ -169,6 +178,9 @@ def run_wgrad(ops, dY, X, out, geom, creal, pro=None, dpro=None):
     if v is None:
         cands = [v for v in range(ops.wgrad_nvariants())
                  if ops.wgrad_variant_ok(v, geom, psc is not None, dpro is not None)]
+        if concurrent:
+            cands = [c for c in cands
+                     if ops.wgrad_variant_area(c) <= CONCURRENT_MAX_TILE] or cands
         v = tuning.pick(key, cands, 1 if N <= 64 else 0,
                         lambda vv: launch(vv, torch.empty_like(out), trial=True))
     launch(v, out)
