@@ -125,7 +125,10 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
   const int64_t M = (int64_t)g.Nb * g.OH * g.OW;
   const int bm = igemm_variant_bm((int)variant);
-  const bool dual = pro_out.has_value() && pro_out->defined();
+  const bool has_pd = pro_d.has_value() && pro_d->defined();
+  // pro_out: the block-output prologue's output (dual) — or, with the BN-backward prologue on a
+  // patch variant, the materialised prologue result (the weight gradient's dY)
+  const bool dual = pro_out.has_value() && pro_out->defined() && !has_pd;
   if (dual) {
     TORCH_CHECK(igemm_dual_ok((int)variant, g),
                 "igemm: block-output prologue needs a 2-stage LDS-DMA variant (igemm_dual_ok) on "
@@ -219,6 +222,20 @@ void igemm(const Tensor& A, const Tensor& B, const Tensor& out, const c10::optio
                 "igemm BN-backward prologue: epilogue 0, 3 or 4");
     f.pro_d = f32(*pro_d, "pro_d");
     f.A2 = bf(*A2, "A2");
+    if (pro_out.has_value() && pro_out->defined()) {
+      TORCH_CHECK(igemm_variant_patch((int)variant) && (epi_mode == 0 || epi_mode == 3),
+                  "igemm: the materialised BN-backward operand (pro_out) needs a patch variant "
+                  "and epilogue 0 or 3");
+      TORCH_CHECK(pro_out->numel() == A.numel(), "igemm: pro_out must match A");
+      const char* o0 = static_cast<const char*>(pro_out->data_ptr());
+      const char* o1 = o0 + pro_out->numel() * 2;
+      for (const Tensor* t : {&A, &*A2, &out}) {
+        const char* t0 = static_cast<const char*>(t->data_ptr());
+        const char* t1 = t0 + t->numel() * t->element_size();
+        TORCH_CHECK(!(o0 < t1 && t0 < o1), "igemm: pro_out must not alias A, A2 or out");
+      }
+      f.pro_out = bfw(*pro_out, "pro_out");
+    }
   }
   if (dual) {
     TORCH_CHECK(f.pro_sc && f.pro_sh && !f.pro_d && epi_mode == 0 && !(bias.has_value() && bias->defined()),
@@ -945,6 +962,9 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_glds_ok(int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_gldsok);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
   m.def("wgrad_variant_glds(int v) -> bool", &wgrad_vglds);
+  m.def("igemm_variant_patch(int v) -> bool", [](int64_t v) {
+    return v >= 0 && v < igemm_num_variants() && igemm_variant_patch((int)v);
+  });
   m.def("wgrad_variant_area(int v) -> int", [](int64_t v) -> int64_t {
     TORCH_CHECK(v >= 0 && v < wgrad_num_variants(), "wgrad variant out of range");
     return wgrad_variant_area((int)v);

@@ -948,6 +948,9 @@ __global__ __launch_bounds__(64 * WM * WN, NST == 1 ? 2 : 1) void igemm_glds(Ige
 // Host guarantees (igemm_variant_ok): KH = KW = 3, unit strides, ih0 = iw0 = -1, OH = IH,
 // OW = IW in {16, 32}, C in {64, 128}, direct output; PRO 1: BN-apply + ReLU on the landed
 // patch, padding kept zero.
+// PRO 2 (BatchNorm-backward operand prologue): patch chunks per thread, at most — the second
+// operand is held in registers (host: ceil(patch pixels x C/8 / threads) <= this)
+constexpr int kPatchBnbChunks = 11;
 template <int BN, int WM, int WN, int EPI, int PRO>
 __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
   constexpr int BM = 256;
@@ -986,7 +989,17 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
   // shift pairs are loaded once, before the DMA (a global load consumed after it would drain
   // it), and the pixel walk is incremental (no per-chunk division by the patch width)
   f32x2 psc2[4], psh2[4];
-  if (PRO) {
+  float pa[8], pb[8], pd[8];  // PRO 2: the BatchNorm-backward coefficients of the thread's chunk
+  if (PRO == 2) {
+    const int pseg = m0 / p.pro_seg_rows;
+    const int ch = ((tid % CPP) ^ ((tid / CPP) & 7)) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pa[e] = p.pro_sc[pseg * C + ch + e];
+      pb[e] = p.pro_sh[pseg * C + ch + e];
+      pd[e] = p.pro_d[pseg * C + ch + e];
+    }
+  } else if (PRO) {
     const int pseg = m0 / p.pro_seg_rows;  // block-uniform (host guarantees)
     const int ch = ((tid % CPP) ^ ((tid / CPP) & 7)) * 8;
     const float4* ps = (const float4*)(p.pro_sc + pseg * C + ch);
@@ -1007,6 +1020,25 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
         ok ? (uint32_t)((((img * p.IH + ih) * p.IW + iw) * C + lch * 8) * 2) : p.a_bytes;
     dma16(ra, Ps + i * 512, off);  // 512 elements = 1 KiB per instruction
   }
+  // PRO 2: the second BatchNorm-backward operand (the pre-BN activation) of every chunk this
+  // thread transforms, loaded to registers under the patch DMA (host: <= kPatchBnbChunks each)
+  u32x4 a2v[kPatchBnbChunks];
+  if (PRO == 2) {
+    const __amdgpu_buffer_rsrc_t r2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.A2, (short)0, (int)p.a_bytes, 0x00020000);
+    const int QS = NT / CPP, q0 = tid / CPP;
+    const int lch = (tid % CPP) ^ (q0 & 7);  // the same logical chunk for every i (QS % 8 == 0)
+#pragma unroll
+    for (int i = 0; i < kPatchBnbChunks; ++i) {
+      const int q = q0 + i * QS;
+      const int pr = q / PW, pc = q - (q / PW) * PW;
+      const int ih = row0 - 1 + pr, iw = pc - 1;
+      const bool ok = q < PP && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      const uint32_t off =
+          ok ? (uint32_t)((((img * p.IH + ih) * p.IW + iw) * C + lch * 8) * 2) : p.a_bytes;
+      a2v[i] = __builtin_amdgcn_raw_buffer_load_b128(r2, off, 0, 0);
+    }
+  }
   // ---- weight tiles
   const int lrow = lane >> 3, lbch = (lane & 7) ^ (lane >> 3);
   uint32_t b_off[BI];
@@ -1021,6 +1053,36 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
       dma16(rb, Bs + buf * BN * 64 + (j * NW + wid) * 8 * 64, b_off[j] + (uint32_t)(kt * 64) * 2u);
   };
 
+  if (PRO == 2) {
+    // before the accumulators and the epilogue prefetch exist (their registers and the held
+    // second operand are never live together): weight tile 0 joins the patch in flight, then
+    // the BatchNorm backward A·g + B·a + D of the conv's own output gradient, once per patch
+    // pixel on the landed patch (padding stays zero); the block's own pixels of it are also
+    // the materialised gradient the weight gradient reads (pro_out, column-0 blocks only)
+    issue_b(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch + second operand + weight tile 0
+    __builtin_amdgcn_s_barrier();
+    const int QS = NT / CPP, q0 = tid / CPP;
+    const int lch = (tid % CPP) ^ (q0 & 7);
+    uint16_t* base = Ps + tid * 8;
+    const bool store = p.pro_out != nullptr && nb == 0;
+#pragma unroll
+    for (int i = 0; i < kPatchBnbChunks; ++i) {
+      const int q = q0 + i * QS;
+      const int pr = q / PW, pc = q - (q / PW) * PW;
+      const int ih = row0 - 1 + pr, iw = pc - 1;
+      const bool ok = q < PP && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      if (ok) {
+        const u32x4 w = bnbwd8(*(const u32x4*)(base + (size_t)i * NT * 8), a2v[i], pa, pb, pd,
+                               true);
+        *(u32x4*)(base + (size_t)i * NT * 8) = w;
+        if (store && pr >= 1 && pr <= TR)
+          *(u32x4*)(p.pro_out + (((size_t)img * p.IH + ih) * p.IW + iw) * C + lch * 8) = w;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -1038,13 +1100,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_patch(IgemmArgs p) {
   EpiBatch<epi_unr<BM, BN, NT>()> pre;
   if (epi_prefetch<EPI>()) epi_load_batch<BM, BN, NT, EPI>(p, m0, n0, 0, pre);
   const int nk = p.K / 64;
-  issue_b(0, 0);
+  if (PRO != 2) issue_b(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch (first step) + weight tile kt
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (PRO && kt == 0) {
+    if (PRO == 1 && kt == 0) {
       // the previous BatchNorm's normalise + ReLU, once per patch pixel on the landed patch
       // (no DMA in flight here); the zero padding of out-of-image pixels stays exactly zero.
       // Four chunks per batch: their LDS reads are all issued before the first write-back.
@@ -2454,6 +2516,13 @@ void launch_patch_t(const IgemmArgs& a0, hipStream_t s) {
 
 template <int BN, int WM, int WN>
 void launch_patch(const IgemmArgs& a, hipStream_t s) {
+  if (a.pro_d != nullptr) {  // BN-backward prologue on the landed patch: plain or mode-3 epilogue
+    if (a.epi_mode == 3)
+      launch_patch_t<BN, WM, WN, 3, 2>(a, s);
+    else
+      launch_patch_t<BN, WM, WN, 0, 2>(a, s);
+    return;
+  }
   if (a.pro_sc != nullptr) {  // BN-apply prologue on the landed patch, any epilogue
     switch (a.epi_mode) {
       case 1: launch_patch_t<BN, WM, WN, 1, 1>(a, s); break;
@@ -2954,6 +3023,7 @@ bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   // zero-padding taps
   return !(pro || bn_bwd_pro) || (g.KH == 1 && g.KW == 1 && g.ih0 == 0 && g.iw0 == 0);
 }
+bool igemm_variant_patch(int v) { return v >= IG_PATCH0 && v < IG_GLDS8W; }
 bool igemm_patch_ok(const ConvGeom& g) {
   const bool direct = g.osh == 1 && g.osw == 1 && g.ooh == 0 && g.oow == 0 && g.OHp == g.OH &&
                       g.OWp == g.OW;
@@ -2983,8 +3053,15 @@ bool igemm_variant_is_patch(int v) { return v >= IG_PATCH0 && v < IG_GLDS8W; }
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro) {
   if (v < 0 || v >= igemm_num_variants()) return false;
   if (v < IG_GLDS0) return true;  // register-staged kernel: every geometry and fusion
-  // patch kernel: BN-apply prologue but no BN-backward one
-  if (v >= IG_PATCH0 && v < IG_GLDS8W) return !bn_bwd_pro && igemm_patch_ok(g);
+  // patch kernel: BN-apply prologue, or the BN-backward one while its second operand fits the
+  // per-thread register stage (kPatchBnbChunks chunks of the patch per thread)
+  if (v >= IG_PATCH0 && v < IG_GLDS8W) {
+    if (!igemm_patch_ok(g)) return false;
+    if (!bn_bwd_pro) return true;
+    const int NT = v == IG_PATCH0 ? 256 : 512;  // launch_patch<64, 4, 1> / <128, 4, 2>
+    const int TR = 256 / g.OW, PP = (TR + 2) * (g.OW + 2);
+    return (PP * (g.C / 8) + NT - 1) / NT <= kPatchBnbChunks;
+  }
   if (v >= IG_GLDS1) return !bn_bwd_pro && igemm_glds_ok(g, pro, false);
   if (v >= IG_GLDS3 && v < IG_PATCH0 && (pro || bn_bwd_pro)) return false;
   if (bn_bwd_pro) {  // PRO 2 stages dY and x: doubled A staging + a 3 x C table must fit
@@ -3021,9 +3098,10 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
   a.epi_ss = f.epi_ss; a.epi_mi = f.epi_mi; a.epi_S = f.epi_S > 0 ? f.epi_S : 1;
   a.seg_rows = f.seg_rows; a.stats_seg_blocks = f.stats_seg_blocks; a.stats_base = f.stats_base;
   if (variant < 0 || variant >= igemm_num_variants()) variant = igemm_default_variant(g.N);
-  if (a.pro_out != nullptr
-          ? !igemm_dual_ok(variant, g)
-          : !igemm_variant_ok(variant, g, a.pro_sc != nullptr, a.pro_d != nullptr)) {
+  const bool dual = a.pro_out != nullptr && a.pro_d == nullptr;  // (with pro_d: materialised
+                                                                 //  BN-backward operand, patch)
+  if (dual ? !igemm_dual_ok(variant, g)
+           : !igemm_variant_ok(variant, g, a.pro_sc != nullptr, a.pro_d != nullptr)) {
     fprintf(stderr, "igemm: LDS-DMA variant %d: unsupported geometry / prologue\n", variant);
     abort();  // the bindings reject this; never silently change BM (stats layout)
   }

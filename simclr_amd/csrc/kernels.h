@@ -63,7 +63,9 @@ bool igemm_glds_ok(const ConvGeom& g, bool pro, bool bn_bwd_pro);
 // the bindings' checks and the Python autotuner's candidate lists)
 bool igemm_variant_is_patch(int v);
 bool igemm_variant_ok(int v, const ConvGeom& g, bool pro, bool bn_bwd_pro);
-bool igemm_dual_ok(int v, const ConvGeom& g);  // block-output prologue (see igemm_glds)
+bool igemm_dual_ok(int v, const ConvGeom& g);
+bool igemm_variant_patch(int v);  // the LDS-resident-patch 3x3 kernel
+bool igemm_patch_ok(const ConvGeom& g);  // block-output prologue (see igemm_glds)
 int igemm_block_m(int N);
 void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const uint16_t* B,
                    uint16_t* out, const float* bias, float* stats, const ConvFusion& f,

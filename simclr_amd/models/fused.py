@@ -162,6 +162,10 @@ class FusedStages:
         # (layer2.0, register-staged weight gradient) neutral to worse (r4 optimisation log)
         self.lazy_bn3_ds = True
         self._lazy_bn3_ds_dual_only = True
+        # a 3x3 stride-1 conv2's output-gradient BatchNorm backward (BN2) in its patch-kernel
+        # dgrad prologue, which also stores it for the weight gradient: one pass instead of a
+        # bn_bwd_apply pass plus the dgrad's re-read (layer1 / layer2; _patch_bnb_ok)
+        self.patch_bnb = os.environ.get("SIMCLR_PATCH_BNB", "1") != "0"
         # weight gradients on a second stream (forked after each conv's dY is final, joined at
         # the end of the backward): they only feed the flat gradient buffer, so they overlap the
         # dgrad / BatchNorm chain that the next layer's gradient depends on
@@ -534,6 +538,25 @@ class FusedStages:
         xin, pro_ss = tp.ins[L]
         return self._bwd1x1_ok(b.convs[L], aL, xin, pro_ss, tp.acts[L - 1], S)
 
+    def _patch_bnb_ok(self, ops, cs: _ConvSpec, a: torch.Tensor, S: int) -> bool:
+        """Can conv ``cs`` (output ``a``) take its output gradient's BatchNorm backward in the
+        dgrad prologue of the LDS-resident-patch kernel (3x3 / stride 1 / pad 1, the second
+        operand fits the kernel's register stage) and store it for the weight gradient?"""
+        if not (self.patch_bnb and a.is_cuda and cs.k == 3 and cs.stride == 1 and cs.pad == 1):
+            return False
+        Nb, H, W, C = a.shape
+        M = Nb * H * W
+        if M % S or (M // S) % 256:
+            return False
+        Ci = cs.conv.in_channels
+        key = (Nb, H, W, C, Ci)
+        cache = self.__dict__.setdefault("_patch_bnb_cache", {})
+        if key not in cache:
+            g = [Nb, H, W, C, H, W, 3, 3, 1, 1, 1, 1, -1, -1, Ci, H, W, 1, 1, 0, 0, Ci]
+            cache[key] = any(ops.igemm_variant_patch(v) and ops.igemm_variant_ok(v, g, True, True)
+                             for v in range(ops.igemm_nvariants()))
+        return cache[key]
+
     def _lazy_bn1_ok(self, b: _BlockSpec, a1: torch.Tensor, S: int) -> bool:
         """BN1's backward applied in conv1's dgrad / weight-gradient operand prologues instead
         of a materialising pass (a bottleneck's 1x1 stride-1 conv1)."""
@@ -545,7 +568,7 @@ class FusedStages:
     def _dgrad(self, ops, dyn, cs: _ConvSpec, in_shape, S: int, accumulate: bool = False,
                dx: Optional[torch.Tensor] = None, bn_epi: Optional[Tuple] = None,
                bnb: Optional[Tuple] = None, compact: bool = False,
-               sub_resid: bool = False):
+               sub_resid: bool = False, bnb_out: Optional[torch.Tensor] = None):
         """dx (NHWC) = conv-transpose(dy).  ``accumulate``: dx += result (dx must be given).
 
         ``bn_epi`` selects a BatchNorm-backward epilogue that also returns Σg, Σg·x̂ partials
@@ -557,8 +580,9 @@ class FusedStages:
                                           its last pre-BN activation; resid may alias dx); with
                                           ``ad`` (the producer's downsample pre-BN activation)
                                           the partials of its downsample BN too → (p3, pd)
-        ``bnb = (a, coef)`` (1x1 stride-1 only): the A operand is the BatchNorm backward
-        coef.A·dyn + coef.B·a + coef.D computed in the prologue.
+        ``bnb = (a, coef)`` (1x1 stride-1; 3x3 stride-1 on the patch kernel with ``bnb_out``):
+        the A operand is the BatchNorm backward coef.A·dyn + coef.B·a + coef.D computed in the
+        prologue; ``bnb_out`` receives that operand (the weight gradient's dY).
         ``compact`` (stride-2 1x1, pad 0): return the dgrad only at the even input positions, as
         a dense [N, ceil(H/2), ceil(W/2), Ci] tensor (one stride-1 GEMM, no zero fill).
         ``sub_resid``: the residual (``dx`` with ``accumulate``, or bn_epi's resid) is such a
@@ -637,14 +661,14 @@ class FusedStages:
         chosen = []
         bpro = None
         if bnb is not None:
-            assert cs.stride == 1 and cs.k == 1 and len(launches) == 1
+            assert cs.stride == 1 and len(launches) == 1 and (cs.k == 1 or bnb_out is not None)
             SC = S * dyn.shape[-1]
             c = bnb[1]
             bpro = (c[:SC], c[SC:2 * SC], c[2 * SC:], launches[0][2] // S, bnb[0])
         for wt, g, M in launches:
             seg = M // S
             v = igemm_choose(ops, dyn, wt, dx, g, want_stats=True, epi=epi, seg_rows=seg,
-                             epi_tables=tables, bnb=bpro)
+                             epi_tables=tables, bnb=bpro, patch_only=bnb_out is not None)
             chosen.append((wt, g, M, seg, ops.igemm_variant_bm(v), v))
         seg_blocks = sum(seg // bm for (_, _, _, seg, bm, _) in chosen)
         partial = torch.empty((S * seg_blocks * 2 * Ci,), device=dev, dtype=torch.float32)
@@ -655,7 +679,8 @@ class FusedStages:
         base = 0
         for wt, g, M, seg, bm, v in chosen:
             igemm_launch(ops, dyn, wt, dx, g, v, stats=partial, epi=epi, seg_rows=seg,
-                         epi_tables=tables, remap=(seg_blocks, base), second=second, bnb=bpro)
+                         epi_tables=tables, remap=(seg_blocks, base), second=second, bnb=bpro,
+                         bnb_out=bnb_out)
             base += seg // bm
         if partial2 is not None:
             return dx, (partial, partial2), seg_blocks
@@ -982,13 +1007,26 @@ class FusedStages:
         # conv chain, last to first: dgrad (+ BN-bwd partials) → start BN all-reduce → wgrad →
         # finish BN → apply
         lazy0 = None
+        pend = None  # (g, a, coef): the BN backward feeding conv i, left to its patch dgrad
         for i in range(L, 0, -1):
             cs = b.convs[i]
             xin, pro_ss = tp.ins[i]
             a_prev, bs_prev = tp.acts[i - 1], tp.bns[i - 1]
             _ext.TAG = f"{b.name} conv{i + 1} dgrad"
             dyn, bnb = (g3, lazy) if (i == L and lazy is not None) else (da, None)
-            if self._bwd1x1_ok(cs, dyn, xin, pro_ss, a_prev, S):
+            if pend is not None:
+                # dgrad with the BN backward in its patch prologue; that operand is stored as
+                # the weight gradient's dY on the way (no separate bn_bwd_apply pass)
+                gsrc, a_b, coef_b = pend
+                pend = None
+                dy_m = torch.empty_like(a_b)
+                gm, part, nb = self._dgrad(ops, gsrc, cs, a_prev.shape, S,
+                                           bn_epi=("mask", a_prev, bs_prev), bnb=(a_b, coef_b),
+                                           bnb_out=dy_m)
+                h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
+                _ext.TAG = f"{b.name} conv{i + 1} wgrad"
+                self._wgrad(ops, dy_m, xin, cs, pro_ss, S)
+            elif self._bwd1x1_ok(cs, dyn, xin, pro_ss, a_prev, S):
                 _ext.TAG = f"{b.name} conv{i + 1} dgrad+wgrad"
                 gm, part, nb = self._bwd1x1_fused(ops, dyn, bnb, cs, a_prev, bs_prev, S)
                 h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
@@ -1003,6 +1041,9 @@ class FusedStages:
             if i == 1 and prev is not None and self._lazy_bn1_ok(b, a_prev, S):
                 lazy0 = (a_prev, coef)  # da1 never materialised: conv1's operand prologues
                 da = gm
+                continue
+            if i - 1 >= 1 and self._patch_bnb_ok(ops, b.convs[i - 1], a_prev, S):
+                pend = (gm, a_prev, coef)
                 continue
             da_next = torch.empty_like(a_prev)
             ops.bn_bwd_apply(gm, None, a_prev, coef, S, False, da_next, None)

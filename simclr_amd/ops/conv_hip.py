@@ -26,7 +26,8 @@ from . import _ext, tuning
 
 
 def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, epi=None,
-                 seg_rows: int = 0, epi_tables=None, bnb=None, dual=None) -> int:
+                 seg_rows: int = 0, epi_tables=None, bnb=None, dual=None,
+                 patch_only: bool = False) -> int:
     """Autotuned tile variant for this problem (admissible: BM divides the segment rows /
     M whenever per-segment prologue, statistics or the mode-3 epilogue need block-uniform
     segments).  ``dual = (res, rss, out, mask)``: block-output prologue (see igemm_launch)."""
@@ -42,7 +43,7 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ess, emi = epi_tables if epi_tables is not None else (None, None)
     key = ("igemm", tuple(geom), want_stats, psc is not None, emode, bias is not None, seg_rows,
-           bnb is not None, dual is not None)
+           bnb is not None, dual is not None, patch_only)
     hit = tuning.cached(key)
     if hit is not None:  # steady state: no per-launch walk over the variant table
         return hit
@@ -63,6 +64,8 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
             continue
         if seg_rows and seg_rows % bm:
             continue
+        if patch_only and not ops.igemm_variant_patch(v):
+            continue  # (the materialised BN-backward operand exists only in the patch kernel)
         cands.append(v)
     if not cands:
         raise ValueError(f"no igemm tile variant admissible for M={M} segment rows "
@@ -90,13 +93,14 @@ def igemm_choose(ops, A, B, out, geom, bias=None, want_stats=False, pro=None, ep
 
 def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=None,
                  seg_rows: int = 0, epi_tables=None, remap=(0, 0), second=None,
-                 bnb=None, dual=None) -> None:
+                 bnb=None, dual=None, bnb_out=None) -> None:
     """``second = (c2, mi2, stats2)``: mode-4 second BatchNorm stream (see conv.hip);
     ``bnb = (coefA, coefB, coefD, seg_rows, A2)``: BatchNorm-backward A-operand prologue;
     ``dual = (res, rss, out, mask)``: block-output prologue — A is a block's pre-BN conv3
     activation, ``pro`` its BN scale/shift, ``res`` the residual (``rss`` its BN [2][S][C] table
     or None for identity); the conv consumes relu(bn(A) + res') and also writes it to ``out``
-    with its ReLU bitmask ``mask``."""
+    with its ReLU bitmask ``mask``.  ``bnb_out``: with ``bnb`` on a patch variant, the
+    BatchNorm-backward operand is also written there (the weight gradient's dY)."""
     psc, psh, pseg, prelu = pro if pro is not None else (None, None, 0, False)
     pd, A2 = None, None
     if bnb is not None:
@@ -104,6 +108,8 @@ def igemm_launch(ops, A, B, out, geom, v, bias=None, stats=None, pro=None, epi=N
     rss, pout, pmask = None, None, None
     if dual is not None:
         A2, rss, pout, pmask = dual
+    if bnb_out is not None:  # patch kernels: the BN-backward operand also stored (wgrad's dY)
+        pout = bnb_out
     emode, ea, eb = epi[:3] if epi is not None else (0, None, None)
     ec = epi[3] if epi is not None and len(epi) > 3 else None
     em = epi[4] if epi is not None and len(epi) > 4 else None

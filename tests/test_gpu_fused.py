@@ -426,3 +426,50 @@ def test_wgrad_dy_prologue_split_straddles_views(ops, splits):
         assert _rel(out, ref) < 1e-2, (v, splits)
         seen += 1
     assert seen >= 2
+
+
+@pytest.mark.parametrize("N,H,C", [(8, 32, 64), (8, 16, 128)])
+def test_patch_bn_backward_prologue(ops, N, H, C):
+    """The 3x3 dgrad with its output gradient's BatchNorm backward in the patch kernel's
+    prologue (and that operand stored for the weight gradient, ``bnb_out``) vs the separate
+    ``bn_bwd_apply`` pass followed by the plain dgrad: the stored operand matches the pass to
+    the bf16 ulp, the input gradient and its BatchNorm partials within bf16 rounding."""
+    from simclr_amd.models.fused import FusedStages, _BNState, _ConvSpec
+    torch.manual_seed(4)
+    S = 2
+    conv = torch.nn.Conv2d(C, C, 3, 1, 1, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(_bf(torch.randn_like(conv.weight) / math.sqrt(C * 9)).float())
+    g = _bf(torch.randn(N, H, H, C, device=DEV))        # masked gradient w.r.t. BN2's output
+    a2 = _bf(torch.randn(N, H, H, C, device=DEV))       # conv2's pre-BN output
+    coef = (torch.randn(3 * S * C, device=DEV) * 0.5).contiguous()
+    a1 = _bf(torch.randn(N, H, H, C, device=DEV))       # conv2's input producer (BN1 + ReLU)
+    sc = torch.rand(S, C, device=DEV) + 0.5
+    sh = torch.randn(S, C, device=DEV) * 0.3
+    mean = torch.randn(S, C, device=DEV) * 0.2
+    inv = torch.rand(S, C, device=DEV) + 0.5
+    bs = _BNState(torch.cat([mean, inv]).reshape(-1).contiguous(),
+                  torch.stack([sc, sh]).reshape(2, S * C).contiguous(), 1.0)
+    ex = FusedStages.__new__(FusedStages)
+    ex.patch_bnb = True
+    cs = _ConvSpec(conv, None, 1, 3, 1)
+    assert ex._patch_bnb_ok(ops, cs, a2, S)
+    da = torch.empty_like(g)
+    ops.bn_bwd_apply(g, None, a2, coef, S, False, da, None)
+    dx_a, part_a, nb_a = ex._dgrad(ops, da, cs, a1.shape, S, bn_epi=("mask", a1, bs))
+    dy_m = torch.empty_like(g)
+    dx_b, part_b, nb_b = ex._dgrad(ops, g, cs, a1.shape, S, bn_epi=("mask", a1, bs),
+                                   bnb=(a2, coef), bnb_out=dy_m)
+    torch.cuda.synchronize()
+    # the same fp32 formula, but the two kernels' FMA contractions may round a handful of
+    # values to the neighbouring bf16 (measured: 9 / 8 of 0.5 M / 0.26 M elements, 1 ulp; one
+    # of them a cancellation A·g + B·a + D ~ 4e-6 of O(1) terms, 3e-8 apart in fp32)
+    d = (dy_m.float() - da.float()).abs()
+    ulp = torch.maximum(da.float().abs(), dy_m.float().abs()) * 2.0 ** -7
+    assert int((d > 0).sum()) <= d.numel() * 1e-4 and bool((d <= ulp * 1.01 + 1e-6).all())
+    assert _rel(dx_b, dx_a) < 1e-2
+    sa = torch.empty(2 * S * C, device=DEV)
+    sb = torch.empty(2 * S * C, device=DEV)
+    ops.bn_reduce(part_a, nb_a, S, C, sa)
+    ops.bn_reduce(part_b, nb_b, S, C, sb)
+    assert _rel(sb, sa) < 1e-2
