@@ -212,6 +212,9 @@ def run_ours(args, rank, world, dev):
                   file=sys.stderr, flush=True)
             tr.graph = None
             args.graph = False
+    if tr.graph is not None and tr.sreplay is not None and tr.sreplay.pending:
+        _set_mode(tr, tr.graph, "streams")
+        timed(1)  # the executor's planning replay (one serial, per-node timed step)
     if auto and tr.graph is not None and t_eager is not None:
         # execution-mode autotune: eager issue vs replaying the captured step with the HIP graph
         # executor vs the native multi-stream executor over the same captured nodes

@@ -20,6 +20,9 @@
 //   * stream 0 is the caller's current stream; the others fork from it at the start of a replay
 //     and join into it at the end, so a replay is stream-ordered like hipGraphLaunch.
 //
+// gexec_reschedule then re-plans order and streams from measured node durations (list
+// scheduling, see there); the replay path is the same.
+//
 // Host cost per kernel is one hipLaunchKernel with the node's own argument block.  The graph
 // must outlive the executor (torch.cuda.CUDAGraph(keep_graph=True) keeps it).
 #include <ATen/hip/HIPContext.h>
@@ -61,6 +64,7 @@ struct Node {
 
 struct Exec {
   std::vector<Node> nodes;  // issue order
+  std::vector<std::vector<int>> par;  // parents of every node (positions in `nodes`)
   std::vector<hipStream_t> streams;  // [0] is a placeholder: the caller's stream at replay
   std::vector<hipEvent_t> events;
   hipEvent_t fork = nullptr;
@@ -144,6 +148,7 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
 
   auto ex = std::make_unique<Exec>();
   ex->nodes.resize(n);
+  ex->par.assign(n, {});
   const int K = (int)max_streams;
   // ancestor sets as bitsets over topo positions (n is a few thousand at most)
   const size_t words = (n + 63) / 64;
@@ -219,6 +224,7 @@ int64_t gexec_create(int64_t graph_handle, int64_t max_streams) {
     }
     Node& nd = ex->nodes[p];
     nd.stream = s;
+    for (int u : parents[v]) ex->par[p].push_back(pos[u]);
     // waits: parents on other streams that stream s does not already follow
     for (int u : parents[v]) {
       int up = pos[u];
@@ -365,6 +371,184 @@ void gexec_replay(int64_t h) {
   }
 }
 
+// One step issued serially on the caller's stream with a timing event after every node: the
+// per-node durations (µs) for gexec_reschedule.  Executes the step once, like a replay.
+std::vector<double> gexec_timed_replay(int64_t h) {
+  Exec* ex = as_exec(h);
+  hipStream_t cur = at::hip::getCurrentHIPStream().stream();
+  const size_t n = ex->nodes.size();
+  std::vector<hipEvent_t> ev(n + 1);
+  for (auto& e : ev) GX_CHECK(hipEventCreate(&e));
+  GX_CHECK(hipEventRecord(ev[0], cur));
+  for (size_t i = 0; i < n; ++i) {
+    issue(ex->nodes[i], cur);
+    GX_CHECK(hipEventRecord(ev[i + 1], cur));
+  }
+  GX_CHECK(hipEventSynchronize(ev[n]));
+  std::vector<double> d(n);
+  for (size_t i = 0; i < n; ++i) {
+    float ms = 0.f;
+    GX_CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    d[i] = 1e3 * (double)ms;
+  }
+  for (auto e : ev) GX_CHECK(hipEventDestroy(e));
+  return d;
+}
+
+// Re-plan the issue order and the stream of every node from measured node durations (list
+// scheduling): simulate `max_streams` in-order streams, and repeatedly issue, among the nodes whose
+// parents are issued, the one that can start earliest (a cross-stream parent costs `lat_us` of
+// event latency; ties: the longer remaining path to the end of the step, then capture order) on
+// the stream where it starts earliest (ties: the stream of its latest-finishing parent).  The
+// capture-order heuristic of gexec_create queues a node behind an earlier-captured one on its
+// stream even when that one becomes ready much later (e.g. a weight gradient behind one waiting
+// for the dgrad chain); here every stream's order follows the simulated start times.  The busiest
+// stream becomes stream 0.  Waits and events are rebuilt as in gexec_create.
+// The list schedule itself (host-only, no HIP): parents per node in a valid topological order
+// → (issue order, stream per node), the busiest stream renumbered 0.
+void list_schedule(const std::vector<std::vector<int>>& parv, const std::vector<double>& dur,
+                   int K, double lat_us, std::vector<int>& order, std::vector<int>& str) {
+  const int n = (int)parv.size();
+  std::vector<std::vector<int>> ch(n);
+  for (int p = 0; p < n; ++p)
+    for (int u : parv[p]) ch[u].push_back(p);
+  std::vector<double> rank(n, 0.0);
+  for (int p = n; p-- > 0;) {
+    double best = 0.0;
+    for (int c : ch[p]) best = std::max(best, rank[c]);
+    rank[p] = std::max(dur[p], 0.0) + best;
+  }
+  std::vector<double> fin(n, 0.0), freeT(K, 0.0);
+  std::vector<int> npar(n), ready;
+  str.assign(n, -1);
+  order.clear();
+  order.reserve(n);
+  for (int p = 0; p < n; ++p) {
+    npar[p] = (int)parv[p].size();
+    if (!npar[p]) ready.push_back(p);
+  }
+  while (!ready.empty()) {
+    int bi = -1, bk = 0;
+    double bt = 0.0;
+    for (int i = 0; i < (int)ready.size(); ++i) {
+      const int v = ready[i];
+      int pref = -1;
+      double pf = -1.0;
+      for (int u : parv[v])
+        if (fin[u] > pf) { pf = fin[u]; pref = str[u]; }
+      int kk = -1;
+      double tt = 0.0;
+      for (int k = 0; k < K; ++k) {
+        double t = freeT[k];
+        for (int u : parv[v]) t = std::max(t, fin[u] + (str[u] == k ? 0.0 : lat_us));
+        if (kk < 0 || t < tt - 1e-9 || (t <= tt + 1e-9 && k == pref)) { kk = k; tt = t; }
+      }
+      const int b = bi < 0 ? -1 : ready[bi];
+      if (bi < 0 || tt < bt - 1e-9 ||
+          (tt <= bt + 1e-9 && (rank[v] > rank[b] + 1e-9 || (rank[v] >= rank[b] - 1e-9 && v < b)))) {
+        bi = i; bk = kk; bt = tt;
+      }
+    }
+    const int v = ready[bi];
+    ready.erase(ready.begin() + bi);
+    str[v] = bk;
+    fin[v] = bt + std::max(dur[v], 0.0);
+    freeT[bk] = fin[v];
+    order.push_back(v);
+    for (int c : ch[v])
+      if (--npar[c] == 0) ready.push_back(c);
+  }
+  TORCH_CHECK((int)order.size() == n, "graphexec: list schedule lost nodes (not a DAG?)");
+  int used = 1;
+  for (int p = 0; p < n; ++p) used = std::max(used, str[p] + 1);
+  std::vector<int> cnt(used, 0);
+  for (int p = 0; p < n; ++p) cnt[str[p]]++;
+  const int top = (int)(std::max_element(cnt.begin(), cnt.end()) - cnt.begin());
+  if (top != 0)
+    for (int p = 0; p < n; ++p) str[p] = str[p] == top ? 0 : str[p] == 0 ? top : str[p];
+}
+
+void gexec_reschedule(int64_t h, std::vector<double> dur, int64_t max_streams, double lat_us) {
+  Exec* ex = as_exec(h);
+  const int n = (int)ex->nodes.size();
+  TORCH_CHECK((int)dur.size() == n, "graphexec: one duration per node");
+  TORCH_CHECK(max_streams >= 1 && max_streams <= 8, "graphexec: 1..8 streams");
+  std::vector<int> order, str;
+  list_schedule(ex->par, dur, (int)max_streams, lat_us, order, str);
+  int used = 1;
+  for (int p = 0; p < n; ++p) used = std::max(used, str[p] + 1);
+  // rebuild the node list in the new order with waits pruned by vector clocks
+  std::vector<int> npos(n);
+  for (int q = 0; q < n; ++q) npos[order[q]] = q;
+  std::vector<Node> nodes(n);
+  std::vector<std::vector<int>> par(n);
+  std::vector<int> seq(n, 0), slen(used, 0);
+  std::vector<std::vector<int>> clk(used, std::vector<int>(used, 0)), node_clk(n);
+  ex->counts[7] = 0;
+  for (int q = 0; q < n; ++q) {
+    const int v = order[q];
+    Node nd = ex->nodes[v];
+    nd.stream = str[v];
+    nd.waits.clear();
+    nd.event = -1;
+    const int s = nd.stream;
+    for (int u : ex->par[v]) par[q].push_back(npos[u]);
+    for (int up : par[q]) {
+      const int su = nodes[up].stream;
+      if (su == s || clk[s][su] >= seq[up]) continue;
+      nd.waits.push_back(up);
+      for (int k = 0; k < used; ++k) clk[s][k] = std::max(clk[s][k], node_clk[up][k]);
+    }
+    seq[q] = ++slen[s];
+    clk[s][s] = seq[q];
+    node_clk[q] = clk[s];
+    ex->counts[7] += (int64_t)nd.waits.size();
+    nodes[q] = nd;
+  }
+  for (auto e : ex->events) GX_CHECK(hipEventDestroy(e));
+  ex->events.clear();
+  for (auto& nd : nodes)
+    for (int w : nd.waits)
+      if (nodes[w].event < 0) {
+        hipEvent_t e;
+        GX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        nodes[w].event = (int)ex->events.size();
+        ex->events.push_back(e);
+      }
+  // the sub-graph executables move with their nodes (ownership stays with ex->nodes)
+  ex->nodes.swap(nodes);
+  for (auto& nd : nodes) nd.sub = nullptr;
+  ex->par.swap(par);
+  while ((int)ex->streams.size() < used) {
+    hipStream_t st;
+    GX_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    ex->streams.push_back(st);
+    hipEvent_t e;
+    GX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ex->joins.push_back(e);
+  }
+  ex->nstreams = std::max(ex->nstreams, used);
+}
+
+// list_schedule on a DAG given as CSR parent lists (tests): [order..., stream per node...]
+std::vector<int64_t> gexec_list_schedule_op(std::vector<int64_t> off, std::vector<int64_t> parents,
+                                            std::vector<double> dur, int64_t max_streams,
+                                            double lat_us) {
+  const int n = (int)dur.size();
+  TORCH_CHECK((int)off.size() == n + 1 && off[n] == (int64_t)parents.size(), "bad CSR");
+  std::vector<std::vector<int>> parv(n);
+  for (int p = 0; p < n; ++p)
+    for (int64_t i = off[p]; i < off[p + 1]; ++i) {
+      TORCH_CHECK(parents[i] >= 0 && parents[i] < p, "parents must precede their children");
+      parv[p].push_back((int)parents[i]);
+    }
+  std::vector<int> order, str;
+  list_schedule(parv, dur, (int)max_streams, lat_us, order, str);
+  std::vector<int64_t> out(order.begin(), order.end());
+  out.insert(out.end(), str.begin(), str.end());
+  return out;
+}
+
 // [kernels, one-node sub-graphs, memsets, host, empty, event-record, event-wait, cross-stream
 //  waits, streams, recorded events]
 std::vector<int64_t> gexec_stats(int64_t h) {
@@ -396,4 +580,9 @@ TORCH_LIBRARY_FRAGMENT(simclr_amd, m) {
   m.def("gexec_stats(int handle) -> int[]", &gexec_stats);
   m.def("gexec_streams(int handle) -> int[]", &gexec_streams);
   m.def("gexec_destroy(int handle) -> ()", &gexec_destroy);
+  m.def("gexec_timed_replay(int handle) -> float[]", &gexec_timed_replay);
+  m.def("gexec_list_schedule(int[] offsets, int[] parents, float[] durations, int max_streams, "
+        "float lat_us) -> int[]", &gexec_list_schedule_op);
+  m.def("gexec_reschedule(int handle, float[] durations, int max_streams, float lat_us) -> ()",
+        &gexec_reschedule);
 }

@@ -7,7 +7,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_stream_replay_two_stream_dag():
+@pytest.mark.parametrize("sched", ["capture", "list"])
+def test_stream_replay_two_stream_dag(sched):
     from simclr_amd.runtime.graph_exec import StreamReplay
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -32,9 +33,10 @@ def test_stream_replay_two_stream_dag():
         snap = out * 1.0
         zeros = torch.zeros(4096, device=dev)
     g.instantiate()
-    r = StreamReplay(g, max_streams=3)
+    r = StreamReplay(g, max_streams=3, sched=sched)
     st = r.stats()
     assert st["kernels"] >= 5 and st["streams"] >= 2, st
+    assert r.pending == (sched == "list")
     for k in range(3):
         static.copy_(torch.randn(1 << 20, device=dev))
         ref = (static * 2 + 1) ** 2 - (torch.sin(static) * 3 + 1)
@@ -45,6 +47,9 @@ def test_stream_replay_two_stream_dag():
         torch.cuda.synchronize()
         assert torch.equal(out, ref) and torch.equal(snap, ref)
         assert not bool(zeros.any())
+    if sched == "list":  # planned from the timed replay: one duration per node, a valid order
+        assert not r.pending and len(r.durations) == len(r.schedule())
+        assert all(d >= 0.0 for d in r.durations)
     # a long run of back-to-back replays drains (no event / stream leak or hang)
     for _ in range(200):
         r.replay()
@@ -91,11 +96,16 @@ def _trainer(base, stem, batch):
     return Trainer(cfg, st, 512, precision="bf16")
 
 
-@pytest.mark.parametrize("base,stem,batch", [("resnet18", None, 32), ("resnet50", True, 64)])
-def test_stream_replay_matches_graph_replay(base, stem, batch):
+@pytest.mark.parametrize("base,stem,batch,sched", [("resnet18", None, 32, "capture"),
+                                                    ("resnet50", True, 64, "capture"),
+                                                    ("resnet50", True, 64, "list")])
+def test_stream_replay_matches_graph_replay(base, stem, batch, sched, monkeypatch):
     """Two trainers from the same weights, one replaying its captured step with hipGraphLaunch,
     the other with the native multi-stream executor: the same kernels on the same data, so the
-    losses, the fp32 master weights and the BatchNorm running statistics agree bitwise."""
+    losses, the fp32 master weights and the BatchNorm running statistics agree bitwise.  With
+    ``sched="list"`` the executor's first replay is its timed serial planning step and the later
+    ones follow the list schedule (gexec_reschedule)."""
+    monkeypatch.setenv("SIMCLR_REPLAY_SCHED", sched)
     from simclr_amd.data.datasets import synthetic_dataset
     from simclr_amd.data.loader import ContrastiveLoader
     dev = torch.device("cuda", 0)
@@ -123,6 +133,8 @@ def test_stream_replay_matches_graph_replay(base, stem, batch):
     lc = [float(c.step(x).item()) for x in xs[1:]]
     torch.cuda.synchronize()
     assert lb == lc, (lb, lc)
+    if sched == "list":
+        assert not c.sreplay.pending and c.sreplay.durations is not None
     assert torch.equal(b.store.master, c.store.master)
     for (n, u), (_, v) in zip(b.model.named_buffers(), c.model.named_buffers()):
         assert torch.equal(u, v), n
