@@ -65,6 +65,11 @@ def _allreduce(t: torch.Tensor, st, branch: bool = False) -> None:
         dist.all_reduce(t, group=g)
 
 
+def _stage_of(b: "_BlockSpec") -> int:
+    """ResNet stage (1-4) of a block named ``layer<s>.<i>``."""
+    return int(b.name[5]) if b.name.startswith("layer") else 0
+
+
 def _deliver_grad(param: torch.Tensor, compute) -> None:
     """Run ``compute(out)`` writing the fp32 gradient of ``param`` into its flat-store slot
     (and notify the reducer); unbound parameters accumulate into ``param.grad``."""
@@ -900,9 +905,19 @@ class FusedStages:
                 store.producer_streams = [main, self._side]
         g, pre = gout, None
         stem_prev = (self._stem_block, stem_tape) if stem_tape is not None else None
+        hook = getattr(self.resnet, "stage_grads_ready", None) if main is not None else None
         for idx in range(len(self.blocks) - 1, -1, -1):
             prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else stem_prev
             g, pre = self._block_backward(ops, st, S, self.blocks[idx], tapes[idx], g, pre, prev)
+            stage = _stage_of(self.blocks[idx])
+            if hook is not None and stage >= 2 and _stage_of(self.blocks[idx - 1]) != stage:
+                # the stage's first block is done: every weight gradient of the stage is queued
+                # on the side stream and every BN parameter gradient written on this one (its
+                # last BN backward finished at the start of this block): its optimizer update
+                # can run beside the rest of the backward instead of in the step's tail
+                self._side.wait_stream(main)
+                with torch.cuda.stream(self._side):
+                    hook(stage)
         if stem_tape is not None:
             # g = dL/d(stem output)·[y > 0] with the stem BatchNorm's partials from layer1.0's
             # conv1 dgrad epilogue: finish its backward, weight gradient with the BN backward in

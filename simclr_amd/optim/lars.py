@@ -12,12 +12,15 @@ weight_decay=0)`` wrapped in ``apex.parallel.LARC(trust_coefficient=0.001, clip=
 
 GPU path: ``lr_step`` (closed-form schedule on device) → ``lars_norms`` (per-chunk Σp², Σg²) →
 ``lars_update`` (trust ratio, wd fold, momentum, fp32 master, bf16 shadow) — three launches for
-the whole model, no host synchronisation, graph-capturable.  CPU path: the same math in torch
-ops per parameter (the test oracle of the kernels).
+the whole model, no host synchronisation, graph-capturable.  On one GPU the fused executor
+issues the update of stages 4 (+ projection head), 3 and 2 from the backward as soon as their
+gradients are final (``set_early_groups`` / ``early_step``, on its weight-gradient stream), so
+only the layer1 + stem update trails the step.  CPU path: the same math in torch ops per
+parameter (the test oracle of the kernels).
 """
 from __future__ import annotations
 
-from typing import Iterable, List, Optional, Sequence
+from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
 
@@ -53,6 +56,32 @@ def weight_decay_per_param(store: FlatParamStore, weight_decay: float,
     return out
 
 
+class _ChunkTable:
+    """Chunk tables of the LARS kernels over a subset of the store's parameters: chunks in
+    segment order; per-segment chunk ranges index this table (0, 0 outside the subset)."""
+
+    def __init__(self, store: FlatParamStore, idx: Sequence[int], dev):
+        segs = store.segments()
+        cseg, cbeg, cend = [], [], []
+        sbeg, send = [0] * len(segs), [0] * len(segs)
+        for i in idx:
+            o, n = segs[i]
+            sbeg[i] = len(cseg)
+            for b in range(o, o + n, CHUNK):
+                cseg.append(i)
+                cbeg.append(b)
+                cend.append(min(b + CHUNK, o + n))
+            send[i] = len(cseg)
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.nchunks = len(cseg)
+        self.seg = torch.tensor(cseg, **i32)
+        self.beg = torch.tensor(cbeg, **i32)
+        self.end = torch.tensor(cend, **i32)
+        self.seg_beg = torch.tensor(sbeg, **i32)
+        self.seg_end = torch.tensor(send, **i32)
+        self.norms = torch.zeros(max(1, 2 * len(cseg)), device=dev, dtype=torch.float32)
+
+
 class FusedLARS:
     def __init__(self, store: FlatParamStore, weight_decays: Sequence[float], lr0: float,
                  momentum: float = 0.9, nesterov: bool = False, trust_coefficient: float = 0.001,
@@ -82,6 +111,10 @@ class FusedLARS:
                 cend.append(min(b + CHUNK, o + n))
             send.append(len(cseg))
         i32 = dict(device=dev, dtype=torch.int32)
+        self._groups: Dict[int, _ChunkTable] = {}  # early-update groups (set_early_groups)
+        self._rest: Optional[_ChunkTable] = None
+        self._issued: set = set()
+        self.early_issued = 0  # groups issued through early_step (tests / accounting)
         self.chunk_seg = torch.tensor(cseg, **i32)
         self.chunk_beg = torch.tensor(cbeg, **i32)
         self.chunk_end = torch.tensor(cend, **i32)
@@ -119,18 +152,71 @@ class FusedLARS:
     def zero_grad(self, set_to_none: bool = False) -> None:
         self.store.zero_grad()
 
+    def set_early_groups(self, groups: Dict[int, Sequence[int]]) -> None:
+        """Parameter groups (``key`` → indices into ``store.params``) whose update the backward
+        may issue before ``step()`` with ``early_step(key)``, once their gradients are final
+        (the fused executor does so per stage, on its weight-gradient stream, so the update
+        overlaps the rest of the backward instead of trailing it); ``step()`` then updates the
+        groups not issued early and every other parameter.  Same kernels, chunk order and
+        per-segment reduction as the single update: the result is bitwise identical."""
+        dev = self.store.device
+        covered = set()
+        self._groups = {}
+        for key, idx in groups.items():
+            self._groups[int(key)] = _ChunkTable(self.store, sorted(idx), dev)
+            covered |= set(idx)
+        self._rest = _ChunkTable(self.store, [i for i in range(len(self.store.params))
+                                              if i not in covered], dev)
+        self._issued = set()
+
+    def _hip(self) -> bool:
+        m = self.store.master
+        return m.is_cuda and registry.use_hip(m)
+
+    def _launch(self, ops, t: "_ChunkTable") -> None:
+        if t.nchunks == 0:
+            return
+        m = self.store.master
+        ops.lars_norms(m, self.store.grad, t.beg, t.end, self.grad_scale, t.norms)
+        ops.lars_update(m, self.store.grad, self.mom, self.store.shadow, t.seg, t.beg, t.end,
+                        t.seg_beg, t.seg_end, self.seg_wd, self.seg_flags, t.norms, self.lr_t,
+                        self.momentum, self.trust, self.eps, self.grad_scale, self.nesterov)
+
+    def _lr_step(self, ops) -> None:
+        ops.lr_step(self.step_t, self.lr_t, self.lr0, self.warmup, self.total, self.mode)
+
+    def early_step(self, key: int) -> None:
+        """Issue group ``key``'s update now, on the current stream (see set_early_groups)."""
+        if key not in self._groups or key in self._issued or not self._hip():
+            return
+        ops = torch.ops.simclr_amd
+        if not self._issued:
+            self._lr_step(ops)
+        self._issued.add(key)
+        self.early_issued += 1
+        self._launch(ops, self._groups[key])
+
     def step(self) -> None:
         m = self.store.master
         if m.is_cuda and registry.use_hip(m):
             ops = torch.ops.simclr_amd
-            ops.lr_step(self.step_t, self.lr_t, self.lr0, self.warmup, self.total, self.mode)
-            ops.lars_norms(m, self.store.grad, self.chunk_beg, self.chunk_end, self.grad_scale,
-                           self.norms)
-            ops.lars_update(m, self.store.grad, self.mom, self.store.shadow, self.chunk_seg,
-                            self.chunk_beg, self.chunk_end, self.seg_chunk_beg,
-                            self.seg_chunk_end, self.seg_wd, self.seg_flags, self.norms,
-                            self.lr_t, self.momentum, self.trust, self.eps, self.grad_scale,
-                            self.nesterov)
+            if self._rest is None:
+                self._lr_step(ops)
+                ops.lars_norms(m, self.store.grad, self.chunk_beg, self.chunk_end,
+                               self.grad_scale, self.norms)
+                ops.lars_update(m, self.store.grad, self.mom, self.store.shadow, self.chunk_seg,
+                                self.chunk_beg, self.chunk_end, self.seg_chunk_beg,
+                                self.seg_chunk_end, self.seg_wd, self.seg_flags, self.norms,
+                                self.lr_t, self.momentum, self.trust, self.eps,
+                                self.grad_scale, self.nesterov)
+            else:
+                if not self._issued:
+                    self._lr_step(ops)
+                for key, t in self._groups.items():
+                    if key not in self._issued:
+                        self._launch(ops, t)
+                self._launch(ops, self._rest)
+                self._issued = set()
         else:
             self._step_torch()
         self.host_step += 1

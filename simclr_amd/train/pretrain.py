@@ -88,6 +88,7 @@ class Trainer:
                              trust_coefficient=0.001, eps=1e-8, lars=True,
                              schedule_mode=MODE_WARMUP_COSINE, warmup_steps=self.warmup_steps,
                              total_steps=self.total_steps)
+        self._early_updates()
         self.loss_fn = NTXent(temperature=cfg["parameter"]["temperature"],
                               gather=cfg_get(cfg, "loss.gather", False))
         self.hip = self.device.type == "cuda" and registry.use_hip(self.store.master) \
@@ -101,6 +102,27 @@ class Trainer:
         self._static_x = None
         self._static_loss = None
         self.guard = StepGuard(st)
+
+    def _early_updates(self) -> None:
+        """Single GPU: the fused executor issues the optimizer update of stages 4 (with the
+        projection head), 3 and 2 as soon as their gradients are final (FusedLARS.early_step,
+        models/fused.py backward).  With a data-parallel group the gradients are final only
+        after their bucket's all-reduce, so the update stays in step()."""
+        if (self.device.type != "cuda" or self.store.comm
+                or os.environ.get("SIMCLR_EARLY_UPDATE", "1") == "0"):
+            return
+        groups: dict = {}
+        for i, n in enumerate(self.store.names):
+            parts = n.split(".")
+            if parts[0] == "g":
+                groups.setdefault(4, []).append(i)
+            elif len(parts) > 1 and parts[1] in ("layer2", "layer3", "layer4"):
+                groups.setdefault(int(parts[1][5]), []).append(i)
+        backbone = getattr(self.model, "f", None)
+        if not groups or backbone is None:
+            return
+        self.opt.set_early_groups(groups)
+        backbone.stage_grads_ready = self.opt.early_step
 
     def prepare(self, x: torch.Tensor) -> torch.Tensor:
         if self.precision == "bf16" and self.device.type == "cuda":

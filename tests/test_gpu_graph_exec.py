@@ -96,6 +96,39 @@ def _trainer(base, stem, batch):
     return Trainer(cfg, st, 512, precision="bf16")
 
 
+def test_early_stage_updates_match_single_update(monkeypatch):
+    """ResNet-50 CIFAR trainers with and without the per-stage early optimizer updates issued
+    from the fused backward (Trainer._early_updates): the same kernels on the same data, so the
+    losses, master weights and momenta agree bitwise over captured, stream-replayed steps."""
+    from simclr_amd.data.datasets import synthetic_dataset
+    from simclr_amd.data.loader import ContrastiveLoader
+    dev = torch.device("cuda", 0)
+    loader = ContrastiveLoader(synthetic_dataset(512, 10), 64, dev, seed=9)
+    xs = [x.clone() for x, _ in loader][:4]
+    monkeypatch.setenv("SIMCLR_EARLY_UPDATE", "0")
+    a = _trainer("resnet50", True, 64)
+    monkeypatch.setenv("SIMCLR_EARLY_UPDATE", "1")
+    b = _trainer("resnet50", True, 64)
+    assert a.opt._rest is None and b.opt._rest is not None and len(b.opt._groups) == 3
+    with torch.no_grad():
+        b.store.master.copy_(a.store.master)
+        b.store.refresh_shadow()
+        for (_, u), (_, v) in zip(b.model.named_buffers(), a.model.named_buffers()):
+            u.copy_(v)
+    la = [float(a.step(xs[0]).item())]
+    lb = [float(b.step(xs[0]).item())]
+    assert b.opt.early_issued == 3 and b.opt._issued == set()  # issued by the backward
+    for t in (a, b):
+        t.capture(xs[0], warmup=0)
+        t.replay_mode = "streams"
+    la += [float(a.step(x).item()) for x in xs[1:]]
+    lb += [float(b.step(x).item()) for x in xs[1:]]
+    torch.cuda.synchronize()
+    assert la == lb, (la, lb)
+    assert torch.equal(a.store.master, b.store.master)
+    assert torch.equal(a.opt.mom, b.opt.mom)
+
+
 @pytest.mark.parametrize("base,stem,batch,sched", [("resnet18", None, 32, "capture"),
                                                     ("resnet50", True, 64, "capture"),
                                                     ("resnet50", True, 64, "list")])

@@ -204,6 +204,44 @@ def test_lars_kernel_matches_torch(ops):
     assert abs(opts[0].lr_t.item() - opts[1].lr_t.item()) < 1e-6
 
 
+def test_lars_early_groups_bitwise(ops):
+    """The optimizer update split into early groups (issued out of order, on another stream)
+    plus the rest in step() equals the single whole-store update bitwise: same chunks, same
+    per-segment reduction order."""
+    from simclr_amd.models import ContrastiveModel
+    from simclr_amd.optim.lars import FusedLARS, weight_decay_per_param
+    from simclr_amd.parallel.flat import FlatParamStore
+    stores = []
+    for _ in range(2):
+        torch.manual_seed(7)
+        m = ContrastiveModel("resnet18").to(DEV)
+        stores.append(FlatParamStore(m, DEV, shadow_dtype=torch.bfloat16))
+    opts = [FusedLARS(st, weight_decay_per_param(st, 1e-4), lr0=2.0, warmup_steps=3,
+                      total_steps=20) for st in stores]
+    names = stores[1].names
+    groups = {4: [i for i, n in enumerate(names) if ".layer4." in n or n.startswith("g.")],
+              3: [i for i, n in enumerate(names) if ".layer3." in n]}
+    opts[1].set_early_groups(groups)
+    side = torch.cuda.Stream(device=DEV)
+    for k in range(5):
+        g = torch.randn(stores[0].total, device=DEV) * 1e-2
+        for st in stores:
+            st.grad.copy_(g)
+        opts[0].step()
+        side.wait_stream(torch.cuda.current_stream(DEV))
+        with torch.cuda.stream(side):
+            opts[1].early_step(3)
+            if k % 2:
+                opts[1].early_step(4)  # odd steps: group 4 issued early, else left to step()
+        torch.cuda.current_stream(DEV).wait_stream(side)
+        opts[1].step()
+    torch.cuda.synchronize()
+    assert torch.equal(stores[0].master, stores[1].master)
+    assert torch.equal(opts[0].mom, opts[1].mom)
+    assert torch.equal(stores[0].shadow, stores[1].shadow)
+    assert torch.equal(opts[0].lr_t, opts[1].lr_t) and torch.equal(opts[0].step_t, opts[1].step_t)
+
+
 def test_augment_matches_numpy(ops):
     from simclr_amd.data import augment_ref
     rng = np.random.default_rng(0)
