@@ -196,14 +196,23 @@ class Trainer:
         g.instantiate()
         self.graph = g
         self.sreplay = None
+        sched = None
+        if self.st.comm:
+            # with collectives: the capture-order plan, which keeps the gradient all-reduce
+            # chain on a stream of its own (a list schedule planned from one timed replay could
+            # queue chain kernels behind an all-reduce whose duration depends on the other
+            # ranks); single GPU: the list schedule (runtime/graph_exec.py)
+            sched = os.environ.get("SIMCLR_REPLAY_SCHED", "capture")
         if streams < 0:
-            # main chain, weight-gradient stream, downsample branch (+ the gradient all-reduce's
-            # chain at N > 1); at most the 4 hardware queues a process gets (GPU_MAX_HW_QUEUES)
-            streams = 4 if self.st.comm else 3
+            # N > 1: main chain, weight-gradient stream, downsample branch, all-reduce chain (at
+            # most the 4 hardware queues a process gets, GPU_MAX_HW_QUEUES).  N = 1: the list
+            # schedule over 2 streams (chain + one side stream) beat 3 by 0.09-0.26 ms (r5 log):
+            # side work beyond one stream slows the chain more than it overlaps
+            streams = 4 if self.st.comm else 2
         if streams > 0:
             from ..runtime.graph_exec import StreamReplay
             try:
-                self.sreplay = StreamReplay(g, max_streams=streams)
+                self.sreplay = StreamReplay(g, max_streams=streams, sched=sched)
             except RuntimeError as e:  # a node type the executor does not issue: graph only
                 log.warning("multi-stream replay unavailable: %s", e)
                 self.sreplay = None
