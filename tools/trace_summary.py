@@ -1,6 +1,7 @@
 """Summarise a rocprofv3 kernel_trace.csv of a bench run into per-step numbers.
 
-Steps are delimited by the one-per-step ``k_lars_update`` dispatch.  Prints (1) per-kernel
+Steps are delimited by the one-per-step ``k_augment`` dispatch (the step's first kernel; the
+optimizer update is issued per stage since round 5, so ``k_lars_update`` is no longer one per step).  Prints (1) per-kernel
 totals averaged over the last ``--steps`` complete steps and (2) the ordered dispatch list of
 the final step (name, grid, µs) so kernels can be mapped back to layers.
 
@@ -21,7 +22,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--list", action="store_true")
-    ap.add_argument("--marker", default="k_lars_update")
+    ap.add_argument("--marker", default="k_augment")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
