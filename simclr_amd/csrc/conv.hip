@@ -2398,6 +2398,56 @@ __global__ void wgrad_reduce_vec4(const float4* __restrict__ partial, float4* __
     out[i] = s;
   }
 }
+// Small outputs with many splits (e.g. a 64 x 64 1x1 weight gradient split ~250 ways over 2^20
+// rows): the two-level reduction gave each level a few blocks of long per-thread slab walks
+// (67 µs at the very end of the step).  One launch instead: a block owns 16 float4 columns and
+// spreads the slabs over 16 lanes (each thread sums every 16th slab, four loads in flight),
+// then the lanes are combined through LDS in a fixed order (deterministic).
+constexpr int RC_COLS = 16, RC_LANES = 16;
+__global__ __launch_bounds__(256) void wgrad_reduce_cols(const float4* __restrict__ partial,
+                                                         float4* __restrict__ out, int splits,
+                                                         size_t n4, float beta) {
+  __shared__ float4 red[RC_LANES][RC_COLS];
+  const int col = threadIdx.x % RC_COLS, lane = threadIdx.x / RC_COLS;
+  const size_t i = (size_t)blockIdx.x * RC_COLS + col;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, d = a;
+  if (i < n4) {
+    int sp = lane;
+    for (; sp + 3 * RC_LANES < splits; sp += 4 * RC_LANES) {
+      const float4 v0 = partial[(size_t)sp * n4 + i];
+      const float4 v1 = partial[(size_t)(sp + RC_LANES) * n4 + i];
+      const float4 v2 = partial[(size_t)(sp + 2 * RC_LANES) * n4 + i];
+      const float4 v3 = partial[(size_t)(sp + 3 * RC_LANES) * n4 + i];
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      b.x += v1.x; b.y += v1.y; b.z += v1.z; b.w += v1.w;
+      c.x += v2.x; c.y += v2.y; c.z += v2.z; c.w += v2.w;
+      d.x += v3.x; d.y += v3.y; d.z += v3.z; d.w += v3.w;
+    }
+    for (; sp < splits; sp += RC_LANES) {
+      const float4 v = partial[(size_t)sp * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[lane][col] = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
+                               (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
+  __syncthreads();
+  if (lane == 0 && i < n4) {
+    float4 s = red[0][col];
+#pragma unroll
+    for (int l = 1; l < RC_LANES; ++l) {
+      const float4 v = red[l][col];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (beta != 0.f) {
+      const float4 o = out[i];
+      s.x += beta * o.x; s.y += beta * o.y; s.z += beta * o.z; s.w += beta * o.w;
+    }
+    out[i] = s;
+  }
+}
+// the column-parallel form pays where the two-level one has too few blocks
+inline bool reduce_cols_ok(size_t n4, int splits) { return n4 <= 16384 && splits >= 32; }
+
 __global__ void wgrad_reduce_l1(float4* __restrict__ partial, int splits, int group, size_t n4) {
   const int g = blockIdx.y;
   const int s0 = g * group;
@@ -3279,6 +3329,12 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
   const size_t n4 = (size_t)a.N * K / 4;
   int sstride = 1, count = splits;
   constexpr int GROUP = 16;
+  if (Creal == g.C && (a.N * K) % 4 == 0 && reduce_cols_ok(n4, splits)) {
+    hipLaunchKernelGGL(wgrad_reduce_cols, dim3((unsigned)((n4 + RC_COLS - 1) / RC_COLS)),
+                       dim3(256), 0, s, (const float4*)partial, (float4*)out, splits, n4, beta);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   if (splits > 2 * GROUP && (a.N * K) % 4 == 0) {
     const int G = (splits + GROUP - 1) / GROUP;
     int bx = (int)((n4 + 255) / 256);
@@ -3362,6 +3418,12 @@ void wgrad_reduce_slabs(float* partial, int splits, float* out, size_t n, float 
   const size_t n4 = n / 4;
   int sstride = 1, count = splits;
   constexpr int GROUP = 16;
+  if (reduce_cols_ok(n4, splits)) {
+    hipLaunchKernelGGL(wgrad_reduce_cols, dim3((unsigned)((n4 + RC_COLS - 1) / RC_COLS)),
+                       dim3(256), 0, s, (const float4*)partial, (float4*)out, splits, n4, beta);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   if (splits > 2 * GROUP) {
     const int G = (splits + GROUP - 1) / GROUP;
     int bx = (int)((n4 + 255) / 256);

@@ -204,6 +204,25 @@ def test_lars_kernel_matches_torch(ops):
     assert abs(opts[0].lr_t.item() - opts[1].lr_t.item()) < 1e-6
 
 
+@pytest.mark.parametrize("n,splits,beta", [(4096, 32, 0.0), (16384, 257, 0.0), (65536, 100, 1.0),
+                                           (65536, 31, 0.0), (262144, 64, 0.0)])
+def test_wgrad_reduce_slabs_matches_sum(ops, n, splits, beta):
+    """Split-slab reduction (the column-parallel single launch for small outputs with >= 32
+    splits, the two-level one otherwise) vs an fp64 sum; deterministic across launches."""
+    torch.manual_seed(n + splits)
+    part = torch.randn(splits * n, device=DEV)
+    out0 = torch.randn(n, device=DEV)
+    ref = part.view(splits, n).double().sum(0) + beta * out0.double()
+    got = []
+    for _ in range(2):
+        out = out0.clone()
+        ops.wgrad_reduce_slabs(part.clone(), splits, out, beta)
+        got.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(got[0], got[1])
+    assert float((got[0].double() - ref).abs().max()) < 1e-4 * math.sqrt(splits)
+
+
 def test_lars_early_groups_bitwise(ops):
     """The optimizer update split into early groups (issued out of order, on another stream)
     plus the rest in step() equals the single whole-store update bitwise: same chunks, same
