@@ -245,6 +245,36 @@ def run_ours(args, rank, world, dev):
     if tr.graph is not None:
         loader.out = tr._static_x  # the augmentation writes the replayed step's input in place
     loss = None
+    from simclr_amd.parallel import invariant as inv
+    args.dp_invariant = {"dropped_modes": []}
+
+    def replicas(where: str) -> bool:
+        """Data-parallel invariant (parallel/invariant.py): master, shadow, momentum, step
+        counter and BatchNorm buffers bitwise equal on every rank.  Untimed."""
+        if world <= 1:
+            args.dp_invariant[where] = "trivial(1 rank)"
+            return True
+        r = inv.check_replicas(tr.store, tr.opt, tr.model, group=st.group)
+        args.dp_invariant[where] = inv.summary(r)
+        return r["ok"]
+
+    def drop_mode(where: str) -> None:
+        """The replicas diverged under the current issue mode: every rank re-adopts rank 0's
+        state and falls back to eager issue (the same decision everywhere: the check's answer
+        is collective).  Divergence under eager issue is a bug, not a mode problem: raise."""
+        mode = _exec_mode(tr)
+        inv.resync(tr.store, tr.opt, group=st.group)
+        if mode == "eager":
+            raise inv.ReplicaDivergence(f"rank {rank}: replicas diverged under eager issue "
+                                        f"({where}: {args.dp_invariant[where]})")
+        print(f"[bench] rank {rank}: replicas diverged under {mode} replay ({where}); "
+              "dropping it, issuing eagerly", file=sys.stderr, flush=True)
+        args.dp_invariant["dropped_modes"].append(mode)
+        tr.graph = None
+        args.graph = False
+
+    if not replicas("after_probe"):
+        drop_mode("after_probe")
 
     def measure():
         nonlocal loss
@@ -290,6 +320,12 @@ def run_ours(args, rank, world, dev):
         args.graph = False
         args.bn_comm = "rccl(ipc-timeout, re-timed)"
         t0, t1 = measure()
+    if not replicas("after_timed"):
+        # the K timed steps ran on diverged replicas: void; re-time them under eager issue
+        drop_mode("after_timed")
+        t0, t1 = measure()
+        if not replicas("after_retimed"):
+            drop_mode("after_retimed")  # eager diverged: raises
     args.exec_used = _exec_mode(tr)
     if tr.sreplay is not None:
         args.sreplay_stats = tr.sreplay.stats()
@@ -417,6 +453,12 @@ def main(argv=None):
                 base = per_gpu * world
         except Exception:
             base = None
+    flop = None
+    try:
+        from simclr_amd.utils.flops import step_flops
+        flop = step_flops(args.model, True if args.cifar_stem else None, args.size, args.batch)
+    except Exception as e:  # accounting only: never fails the bench
+        print(f"[bench] FLOP count failed: {e!r}", file=sys.stderr, flush=True)
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -457,7 +499,14 @@ def main(argv=None):
             "host_issue_ms_idle_device": (round(args.host_issue_idle_ms, 3)
                                           if hasattr(args, "host_issue_idle_ms") else None),
             "final_loss": loss,
+            "dp_invariant": getattr(args, "dp_invariant", None),
         },
+        # utilisation: model FLOPs of one step per GPU (3 x forward, counted from the real
+        # conv / matmul shapes: simclr_amd/utils/flops.py) over the measured step time
+        "model_tflop_per_step_per_gpu": round(flop / 1e12, 4) if flop else None,
+        "achieved_tflops_per_gpu": round(flop / (ms / 1000.0) / 1e12, 1) if flop else None,
+        "achieved_tflops_total": round(flop * world / (ms / 1000.0) / 1e12, 1) if flop else None,
+        "mfu_vs_2p5pf_dense_bf16": round(flop / (ms / 1000.0) / 2.5e15, 4) if flop else None,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -2398,6 +2398,21 @@ __global__ void wgrad_reduce_vec4(const float4* __restrict__ partial, float4* __
     out[i] = s;
   }
 }
+// In place: slab[i] = Σ_sp slab[sp * step + i] (channel-padded weight gradients reduce into
+// slab 0 before the compaction).  No __restrict__: the output aliases the first slab; each
+// element is read and written by the same thread.
+__global__ void wgrad_reduce_vec4_inplace(float4* slab, int splits, int sstride, size_t n4) {
+  const size_t step = (size_t)sstride * n4;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float4 a = slab[i];
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4 v = slab[(size_t)sp * step + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    slab[i] = a;
+  }
+}
 // Small outputs with many splits (e.g. a 64 x 64 1x1 weight gradient split ~250 ways over 2^20
 // rows): the two-level reduction gave each level a few blocks of long per-thread slab walks
 // (67 µs at the very end of the step).  One launch instead: a block owns 16 float4 columns and
@@ -3357,8 +3372,8 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     // 46 µs at the very end of the backward
     int blocks = (int)((n4 + 255) / 256);
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(wgrad_reduce_vec4, dim3(blocks), dim3(256), 0, s, (const float4*)partial,
-                       (float4*)partial, count, sstride, n4, 0.f);
+    hipLaunchKernelGGL(wgrad_reduce_vec4_inplace, dim3(blocks), dim3(256), 0, s,
+                       (float4*)partial, count, sstride, n4);
     HIP_CHECK_LAUNCH();
     const size_t total = (size_t)a.N * (K / g.C) * Creal;
     int cb = (int)((total + 255) / 256);

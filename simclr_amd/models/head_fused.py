@@ -231,9 +231,27 @@ def _transposed(ops, mod, W1, W2, K, H, D):
     return cache[3].view(K, H), cache[4].view(H, D)
 
 
+def _plan_ready(mod) -> bool:
+    """True when the cached transpose plan (``_transposed``) matches the current bf16 weights.
+    Building a plan uploads a host table; inside a graph capture that upload would become a
+    memcpy node reading a temporary host tensor freed when the capture ends."""
+    s = mod._seq
+    cache = mod.__dict__.get("_head_wt")
+    if cache is None:
+        return False
+    slots = [getattr(w, "_slot", None) for w in (s.linear1.weight, s.linear2.weight)]
+    if any(sl is None or sl.shadow is None for sl in slots):
+        return False  # unbound weights get a fresh bf16 copy (a new pointer) per call
+    return cache[0][:2] == (slots[0].shadow.data_ptr(), slots[1].shadow.data_ptr())
+
+
 def fused_mlp(mod, x: torch.Tensor, segments: int) -> Optional[torch.Tensor]:
-    """The fused head's output, or None when the shapes / mode are not eligible."""
+    """The fused head's output, or None when the shapes / mode are not eligible, or when a
+    graph capture would have to build the weight-transpose plan (the per-op head then runs
+    inside the capture; an eager step before the capture builds the plan)."""
     if not eligible(mod, x, segments):
+        return None
+    if torch.cuda.is_current_stream_capturing() and not _plan_ready(mod):
         return None
     _ext.require()
     s = mod._seq

@@ -8,11 +8,16 @@ events.  That keeps the eager schedule's side-stream concurrency (weight gradien
 dgrad / BatchNorm chain) at ~one ``hipLaunchKernel`` of host time per kernel instead of the ~30 µs
 of Python + dispatcher work of eager issue.
 
-The first replay is a planning step: the nodes run serially with a timing event after each one,
-and the executor re-plans its issue order and stream assignment by list scheduling on those
-durations (every stream ordered by simulated start time, so no node waits behind a later-ready
-one on its stream); at N > 1 every rank plans from rank 0's durations, so the collectives keep
-one issue order across ranks.
+Single GPU (``sched="list"``, the default there): the first replay is a planning step — the
+nodes run serially with a timing event after each one, and the executor re-plans its issue order
+and stream assignment by list scheduling on those durations (every stream ordered by simulated
+start time, so no node waits behind a later-ready one on its stream).
+
+With collectives in the step (N > 1, or a forced 1-rank group) ``Trainer.capture`` keeps the
+capture-order plan (``sched="capture"``): the all-reduce chain stays on a stream of its own and
+every rank issues the collectives in the captured order.  The list schedule is opt-in there
+(``SIMCLR_REPLAY_SCHED=list``); every rank then plans from rank 0's durations (one
+``dist.broadcast`` inside the first replay) so the collectives keep one issue order.
 
 There is no reference counterpart (the reference issues every op eagerly through autograd:
 ``/root/reference/main.py:104-122``); this is the MI355X-native answer to its per-op launch cost.

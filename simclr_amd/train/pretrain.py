@@ -11,10 +11,12 @@ MI355X step (``Trainer.step``), identical math:
   statistics (``segments=2``) on the implicit-GEMM / fused-BN kernels → fused NT-Xent →
   backward with gradients written into the flat fp32 buffer and bucketed RCCL all-reduces on a
   comm stream → ``lr_step`` + fused LARS (no host sync anywhere in the step).
-Optionally the whole step (fwd + bwd + optimizer) is captured once into a hipGraph and replayed
-(``runtime.hip_graph=true``) to remove per-kernel launch overhead: by the native multi-stream
-executor over the captured nodes (``runtime.replay=streams``, runtime/graph_exec.py) or by
-``hipGraphLaunch`` (``runtime.replay=graph``).
+By default (``runtime.hip_graph=auto``) the HIP path runs its first ``GRAPH_AFTER`` steps
+eagerly, then captures the whole step (fwd + bwd + optimizer, collectives included) once into a
+hipGraph and replays it for every later batch — what bench.py measures — to remove per-kernel
+launch overhead: by the native multi-stream executor over the captured nodes
+(``runtime.replay=streams``, runtime/graph_exec.py) or by ``hipGraphLaunch``
+(``runtime.replay=graph``).  ``runtime.hip_graph=false`` issues every step eagerly.
 """
 from __future__ import annotations
 
@@ -40,6 +42,7 @@ from ..ops import registry
 from ..optim.lars import FusedLARS, weight_decay_per_param
 from ..optim.schedule import MODE_WARMUP_COSINE, calculate_initial_lr
 from ..parallel.flat import FlatParamStore
+from ..parallel.invariant import require_replicas
 from ..runtime.dist import init_distributed
 from ..utils.checkpoint import (checkpoint_name, gather_rng_states, load_resume,
                                 save_reference_checkpoint, save_resume)
@@ -260,7 +263,10 @@ def pretrain(cfg) -> dict:
         loader.counter = int(blob["step"])
     max_steps = cfg_get(cfg, "runtime.max_steps", None)
     log_every = int(cfg_get(cfg, "runtime.log_every", 0) or 0)  # progress lines (syncs the step)
-    use_graph = bool(cfg_get(cfg, "runtime.hip_graph", False)) and tr.hip
+    graph_mode = _graph_mode(cfg_get(cfg, "runtime.hip_graph", "auto"))
+    # the captured step cannot hold host (gloo) collectives: a gloo rehearsal stays eager
+    use_graph = (graph_mode != "off" and tr.hip
+                 and (not st.comm or dist.get_backend(st.group) == "nccl"))
     metrics = MetricsWriter("metrics.jsonl" if rank == 0 else None)
     save_every = cfg["experiment"]["save_model_epoch"]
     step_global = tr.opt.host_step
@@ -282,10 +288,24 @@ def pretrain(cfg) -> dict:
                 os._exit(fault[2])
             if prof_win is not None and step_global == prof_win[0] and prof is None:
                 prof = _start_profiler()
-            if use_graph and tr.graph is None:
-                tr.capture(x)
-                tr.replay_mode = str(cfg_get(cfg, "runtime.replay", "streams"))
-                loader.out = tr._static_x  # later batches are augmented in place
+            if use_graph and tr.graph is None and tr.guard.eager_steps >= GRAPH_AFTER:
+                # the first GRAPH_AFTER steps ran eagerly (autotuning, plans, the IPC guard's
+                # tuning steps); this batch's step is the captured one, so every batch is
+                # trained exactly once, as in the eager loop
+                try:
+                    tr.capture(x, warmup=0)
+                except Exception as e:
+                    if graph_mode == "on":
+                        raise
+                    log.warning("hipGraph capture failed (%r): issuing every step eagerly", e)
+                    tr.graph, tr.sreplay, use_graph = None, None, False
+                if tr.graph is not None:
+                    tr.replay_mode = str(cfg_get(cfg, "runtime.replay", "streams"))
+                    loader.out = tr._static_x  # later batches are augmented in place
+                    if rank == 0:
+                        log.info("step %d: training step captured; replay mode %s", step_global,
+                                 "streams" if (tr.replay_mode == "streams"
+                                               and tr.sreplay is not None) else "graph")
             loss = tr.step(x)
             nsteps += 1
             step_global += 1
@@ -301,6 +321,12 @@ def pretrain(cfg) -> dict:
             torch.cuda.synchronize()
         dt = max(time.time() - t0, 1e-9)
         tr.guard.flush(step_global)  # the epoch's last step (its flag copy has landed)
+        if st.world_size > 1:
+            # data-parallel invariant: master, shadow, momentum, step counter and BatchNorm
+            # buffers bitwise equal on every rank (a mis-replayed collective or a rank-local
+            # statistics error would otherwise surface only as a bad accuracy)
+            require_replicas(tr.store, tr.opt, tr.model, group=st.group,
+                             where=f"after epoch {epoch}")
         imgs = nsteps * cfg["experiment"]["batches"] * st.world_size
         summary.update(epochs_run=summary["epochs_run"] + 1, steps=step_global)
         if rank == 0:
@@ -330,6 +356,25 @@ def pretrain(cfg) -> dict:
     summary["wall_seconds"] = time.time() - t_start
     metrics.close()
     return summary
+
+
+# eager steps before the step is captured (runtime.hip_graph auto / true)
+GRAPH_AFTER = 2
+
+
+def _graph_mode(v) -> str:
+    """``runtime.hip_graph``: auto (default: capture + native replay on the HIP path, eager if
+    the capture fails), true (capture, a failure is an error), false (eager issue)."""
+    if isinstance(v, bool):
+        return "on" if v else "off"
+    v = str(v).strip().lower()
+    if v in ("false", "0", "off", "none", "null", "no", "eager"):
+        return "off"
+    if v in ("true", "1", "on", "yes"):
+        return "on"
+    if v == "auto":
+        return "auto"
+    raise ValueError(f"runtime.hip_graph must be auto, true or false, not {v!r}")
 
 
 def _ints(spec):

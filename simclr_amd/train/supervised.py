@@ -30,6 +30,7 @@ from ..ops.classify import ce_rank, cross_entropy
 from ..optim.lars import FusedLARS
 from ..optim.schedule import MODE_WARMUP_COSINE, calculate_initial_lr
 from ..parallel.flat import FlatParamStore
+from ..parallel.invariant import require_replicas
 from ..runtime.dist import init_distributed
 from ..utils.checkpoint import checkpoint_name, save_reference_checkpoint
 from ..utils.misc import MetricsWriter, cfg_get, refuse_experiment_knobs, seed_everything
@@ -139,6 +140,8 @@ def supervised(cfg) -> dict:
                 epoch, epochs, epoch / epochs, float(loss.item()), opt.logged_lr)
         sum_loss, correct = validation(model, val_loader, precision, dev)
         if st.world_size > 1:
+            # every rank must still hold bitwise the same replicated state (ReplicaDivergence)
+            require_replicas(store, opt, model, group=st.group, where=f"after epoch {epoch}")
             dist.barrier()
             dist.reduce(sum_loss, dst=0)
             dist.reduce(correct, dst=0)

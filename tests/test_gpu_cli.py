@@ -30,10 +30,13 @@ def test_gpu_pretrain_graph_eval_resume(tmp_path):
     # fixed tile variants in both processes (runtime.deterministic: autotuner off): timed tile
     # choices can differ between two processes on near-ties, and with them the fp32 summation
     # order — the resume check below is about the checkpointed state, not autotune noise
+    # no runtime.hip_graph override: the default captures the step after 2 eager steps and
+    # replays it with the native multi-stream executor (what bench.py measures)
     out = _run("main.py", COMMON + ["parameter.epochs=2", "parameter.warmup_epochs=1",
-                                    "experiment.save_model_epoch=1", "runtime.hip_graph=true",
+                                    "experiment.save_model_epoch=1",
                                     "runtime.deterministic=true", f"hydra.run.dir={run}"],
                tmp_path)
+    assert "step 2: training step captured; replay mode streams" in out, out[-3000:]
     assert "Epoch:2/2 progress:1.000 loss:" in out
     loss = float([l for l in out.splitlines() if "Epoch:2/2" in l][0].split("loss:")[1].split(",")[0])
     assert loss == loss and 0.0 < loss < 20.0
@@ -46,7 +49,7 @@ def test_gpu_pretrain_graph_eval_resume(tmp_path):
     run2 = tmp_path / "run2"
     out2 = _run("main.py", COMMON + ["parameter.epochs=2", "parameter.warmup_epochs=1",
                                      "experiment.save_model_epoch=1", f"hydra.run.dir={run2}",
-                                     "runtime.deterministic=true",
+                                     "runtime.deterministic=true", "runtime.hip_graph=false",
                                      f"runtime.resume={run / 'resume-1.pt'}"], tmp_path)
     l2 = float([l for l in out2.splitlines() if "Epoch:2/2" in l][0].split("loss:")[1].split(",")[0])
     assert abs(l2 - loss) < 0.05, (loss, l2)

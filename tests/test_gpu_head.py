@@ -138,3 +138,48 @@ def test_fused_head_cuts_launches():
     k_ops = _head_kernels(m, x, R, S, False)
     print("head kernels fused / per-op:", k_fused, k_ops)
     assert k_fused <= 9 and 10 * k_fused <= 6 * k_ops, (k_fused, k_ops)
+
+
+def test_capture_without_warmup_skips_plan_build():
+    """A graph capture that reaches the fused head before any eager step would have to build
+    the weight-transpose plan inside the capture (a host-table upload recorded as a memcpy from
+    a temporary host tensor).  The head then takes the per-op path for that capture; after an
+    eager step has built the plan, a capture uses the fused head.  Both replays match an eager
+    fused step on the same weights."""
+    from simclr_amd.models import head_fused
+    from simclr_amd.parallel import state as pstate
+    from simclr_amd.parallel.flat import FlatParamStore
+    pstate.reset()
+    pstate.get().device = torch.device(DEV, 0)
+    S, n, H, D = 2, 256, 2048, 128
+    m = _head(H, D)
+    store = FlatParamStore(m, torch.device(DEV, 0), shadow_dtype=torch.bfloat16)
+    x = torch.randn(S * n, H, device=DEV).to(torch.bfloat16)
+    assert head_fused.eligible(m, x, S) and not head_fused._plan_ready(m)
+    names = []
+
+    def run():
+        z = m(x, segments=S)
+        names.append(type(z.grad_fn).__name__)
+        return z
+
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g):
+        z_cap = run()
+    g.instantiate()
+    assert not names[-1].startswith("MLPHeadFn"), names
+    assert "_head_wt" not in m.__dict__  # no plan was built inside the capture
+    z_eager = run().detach().clone()  # eager: the fused head, builds the plan
+    assert names[-1].startswith("MLPHeadFn") and head_fused._plan_ready(m)
+    g.replay()
+    torch.cuda.synchronize()
+    assert _rel(z_cap, z_eager) < 1e-2
+    g2 = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g2):
+        z_cap2 = run()
+    g2.instantiate()
+    assert names[-1].startswith("MLPHeadFn")
+    g2.replay()
+    torch.cuda.synchronize()
+    assert _rel(z_cap2, z_eager) < 1e-2
+    del store

@@ -559,3 +559,60 @@ def test_igemm_dgrad_parity_classes_every_variant(ops, k, p, C, Co, H):
         covered[r::2, c::2] = True
     assert bool(covered.all()) or k == 1
     assert seen_glds, "no LDS-DMA variant admitted the parity-class geometry"
+
+
+@pytest.mark.parametrize("k,s,p,H", [(3, 1, 1, 32), (3, 1, 3, 32)])
+def test_wgrad_bn_backward_prologue_padded_channels(ops, k, s, p, H):
+    """The stem's weight gradient as the fused executor runs it: the dY operand is the
+    BatchNorm backward A·dY + B·Y + D of the stem's own BN (per-row view segment, computed in
+    the prologue), the input holds 3 real image channels gathered as 8, and the result is
+    compacted to the 3 real channels (in-place slab sum, then compaction).  Every admissible
+    variant, with split counts aligned to the views and — for the register-staged variants,
+    which take each row's own segment — counts that straddle the view boundary, against torch's
+    fp32 conv2d weight gradient of the same operands."""
+    from simclr_amd.ops.conv_hip import fwd_geom, run_wgrad
+    torch.manual_seed(17)
+    N, C, Creal, Co, S = 16, 8, 3, 64, 2
+    x = _bf(torch.randn(N, C, H, H, device=DEV))
+    y = F.conv2d(x.float()[:, :Creal], torch.randn(Co, Creal, k, k, device=DEV) * 0.3, None, s, p)
+    Y = _bf(y)  # the BN input (pre-BN conv output), stored bf16
+    gy = _bf(torch.randn_like(y))
+    OH, OW = y.shape[-2:]
+    M = N * OH * OW
+    seg = M // S
+    coef = torch.cat([torch.rand(S, Co, device=DEV) + 0.5, torch.randn(S, Co, device=DEV) * 0.2,
+                      torch.randn(S, Co, device=DEV) * 0.1]).reshape(-1).contiguous()
+    A, B, D = coef.view(3, S, Co)
+    segi = torch.arange(N, device=DEV) // (N // S)
+    dy_eff = (A[segi][:, :, None, None] * gy.float() + B[segi][:, :, None, None] * Y.float()
+              + D[segi][:, :, None, None])
+    wr = torch.zeros(Co, Creal, k, k, device=DEV, requires_grad=True)
+    F.conv2d(x.float()[:, :Creal], wr, None, s, p).backward(dy_eff)
+    ref = wr.grad
+    g = fwd_geom(N, H, H, C, OH, OW, k, k, s, p, Co)
+    xn = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    dyn = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    Yn = Y.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+    K = k * k * C
+    vs = [v for v in range(ops.wgrad_nvariants()) if ops.wgrad_variant_ok(v, g, False, True)]
+    assert vs
+    checked = 0
+    for v in vs:
+        cands = {S, 2 * S, S * max(1, ops.wgrad_splits(g, v) // S)}
+        if not ops.wgrad_variant_glds(v):
+            cands |= {1, 3}  # straddling the view boundary
+        for splits in sorted(cands):
+            if splits > 1 and (M // 64) < splits:
+                continue
+            part = torch.full((splits * Co * K,), float("nan"), device=DEV)
+            out = torch.full((Co, k, k, Creal), float("nan"), device=DEV)
+            ops.wgrad(dyn, xn, part, out, g, splits, Creal, 0.0, None, None, 0, False, 1, v,
+                      Yn, coef, seg, S)
+            torch.cuda.synchronize()
+            assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2, (v, splits)
+            checked += 1
+    # the production entry point (autotuned variant, aligned splits)
+    out = torch.empty(Co, k, k, Creal, device=DEV)
+    run_wgrad(ops, dyn, xn, out, g, Creal, dpro=(Yn, coef, seg, S))
+    assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2
+    assert checked >= len(vs)
