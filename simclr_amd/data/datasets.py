@@ -112,11 +112,51 @@ def synthetic_dataset(n: int, num_classes: int = 10, size: int = 32, seed: int =
     return ImageDataset(imgs, labels, num_classes, name, synthetic=True)
 
 
+def synthetic_texture_dataset(n: int, num_classes: int = 10, size: int = 32, seed: int = 0,
+                              name: str = "synthetic-texture", template_seed: int = 4321,
+                              noise: float = 40.0) -> ImageDataset:
+    """A mid-difficulty accuracy proxy (no CIFAR on the machine): the class is a texture — a
+    sum of two oriented sinusoidal gratings with class-specific frequencies / orientations —
+    while everything SimCLR's augmentations randomise is nuisance: a random mean colour per
+    image (colour jitter / grayscale), a random phase and position (crop), a random contrast,
+    plus Gaussian pixel noise (``noise``).  Orientations are chosen flip-symmetric per class
+    (each class holds a grating and its mirror image), so horizontal flips keep the class.
+    A probe must read texture frequency / orientation through noise: random-init features
+    separate it only partly, and pre-training has to learn the invariances
+    (tools/accuracy_proxy.sh, profiles/r6_accuracy_proxy.md)."""
+    g = np.random.default_rng(seed)
+    labels = g.integers(0, num_classes, size=n).astype(np.int64)
+    cg = np.random.default_rng(template_seed)  # shared by the train and test splits
+    freq = cg.uniform(1.5, 5.0, size=(num_classes, 2))       # cycles per image
+    theta = cg.uniform(0.0, np.pi / 2, size=(num_classes, 2))
+    yy, xx = np.meshgrid(np.arange(size) / size, np.arange(size) / size, indexing="ij")
+    imgs = np.empty((n, size, size, 3), dtype=np.uint8)
+    bs = 2048
+    for s in range(0, n, bs):
+        e = min(n, s + bs)
+        m = e - s
+        lab = labels[s:e]
+        acc = np.zeros((m, size, size), dtype=np.float32)
+        for k in range(2):
+            th = theta[lab, k] * np.where(g.random(m) < 0.5, 1.0, -1.0)  # mirror pairs
+            f = freq[lab, k] * g.uniform(0.85, 1.15, size=m)
+            ph = g.uniform(0, 2 * np.pi, size=m)
+            u = (np.cos(th)[:, None, None] * xx[None] + np.sin(th)[:, None, None] * yy[None])
+            acc += np.sin(2 * np.pi * f[:, None, None] * u + ph[:, None, None])
+        amp = g.uniform(18.0, 45.0, size=(m, 1, 1, 1)).astype(np.float32)
+        col = g.uniform(60.0, 195.0, size=(m, 1, 1, 3)).astype(np.float32)
+        tint = g.uniform(0.6, 1.0, size=(m, 1, 1, 3)).astype(np.float32)
+        eps = g.normal(0, noise, size=(m, size, size, 3)).astype(np.float32)
+        img = col + amp * tint * acc[..., None] + eps
+        imgs[s:e] = np.clip(img, 0, 255).astype(np.uint8)
+    return ImageDataset(imgs, labels, num_classes, name, synthetic=True)
+
+
 def load_dataset(name: str, train: bool = True, root: str = DEFAULT_ROOT,
                  synthetic: bool = False, synthetic_size: Optional[int] = None,
                  allow_synthetic_fallback: bool = False, seed: int = 0,
                  image_size: int = 32, synthetic_noise: float = 25.0,
-                 synthetic_colour: bool = True) -> ImageDataset:
+                 synthetic_colour: bool = True, synthetic_kind: str = "template") -> ImageDataset:
     name = name.lower()
     if name not in ("cifar10", "cifar100"):
         raise ValueError("experiment.name must be cifar10 or cifar100, got {!r}".format(name))
@@ -132,6 +172,12 @@ def load_dataset(name: str, train: bool = True, root: str = DEFAULT_ROOT,
                 f"{name} not found under {r} (no network to download it); "
                 "place the CIFAR python/binary batches there or run with data.synthetic=true")
     n = synthetic_size if synthetic_size is not None else (50000 if train else 10000)
+    if synthetic_kind == "texture":
+        return synthetic_texture_dataset(n, ncls, size=image_size,
+                                         seed=seed + (0 if train else 7919),
+                                         name=f"synthetic-texture-{name}", noise=synthetic_noise)
+    if synthetic_kind != "template":
+        raise ValueError(f"data.synthetic_kind must be template or texture, not {synthetic_kind!r}")
     return synthetic_dataset(n, ncls, size=image_size, seed=seed + (0 if train else 7919),
                              name=f"synthetic-{name}", noise=synthetic_noise,
                              colour=synthetic_colour)

@@ -78,6 +78,7 @@ def _datasets(cfg):
               allow_synthetic_fallback=bool(cfg_get(cfg, "data.synthetic_fallback", False)),
               synthetic_noise=float(cfg_get(cfg, "data.synthetic_noise", 25.0)),
               synthetic_colour=bool(cfg_get(cfg, "data.synthetic_colour", True)),
+              synthetic_kind=str(cfg_get(cfg, "data.synthetic_kind", "template")),
               seed=seed)
     size = cfg_get(cfg, "data.synthetic_size", None)
     tr = load_dataset(cfg["experiment"]["name"], train=True,

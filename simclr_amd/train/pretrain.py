@@ -247,6 +247,7 @@ def pretrain(cfg) -> dict:
                       synthetic_size=cfg_get(cfg, "data.synthetic_size", None),
                       synthetic_noise=float(cfg_get(cfg, "data.synthetic_noise", 25.0)),
                       synthetic_colour=bool(cfg_get(cfg, "data.synthetic_colour", True)),
+                      synthetic_kind=str(cfg_get(cfg, "data.synthetic_kind", "template")),
                       allow_synthetic_fallback=bool(cfg_get(cfg, "data.synthetic_fallback", False)),
                       seed=seed)
     loader = ContrastiveLoader(ds, cfg["experiment"]["batches"], st.device, rank=rank,

@@ -76,6 +76,7 @@ def supervised(cfg) -> dict:
               allow_synthetic_fallback=bool(cfg_get(cfg, "data.synthetic_fallback", False)),
               synthetic_noise=float(cfg_get(cfg, "data.synthetic_noise", 25.0)),
               synthetic_colour=bool(cfg_get(cfg, "data.synthetic_colour", True)),
+              synthetic_kind=str(cfg_get(cfg, "data.synthetic_kind", "template")),
               seed=seed)
     size = cfg_get(cfg, "data.synthetic_size", None)
     train_ds = load_dataset(cfg["experiment"]["name"], train=True, synthetic_size=size, **kw)
