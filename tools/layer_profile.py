@@ -78,6 +78,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--size", type=int, default=32)
+    ap.add_argument("--reference-stem", dest="cifar_stem", action="store_false", default=True,
+                    help="the reference's stem (r50: ImageNet 7x7/s2 + maxpool)")
+    ap.add_argument("--model", default="resnet50")
     a = ap.parse_args()
     from simclr_amd.ops import _ext
     from simclr_amd.config import compose, task_config, CONF_DIR
@@ -90,10 +94,11 @@ def main():
     st = pstate.get()
     st.device = dev
     cfg = task_config(compose(str(CONF_DIR), "config", [
-        "experiment.base_cnn=resnet50", "model.cifar_stem=true", f"experiment.batches={a.batch}",
-        "data.synthetic=true", "parameter.epochs=10"]))
+        f"experiment.base_cnn={a.model}", f"model.cifar_stem={'true' if a.cifar_stem else 'null'}",
+        f"experiment.batches={a.batch}", "data.synthetic=true", "parameter.epochs=10"]))
     tr = Trainer(cfg, st, 50000)
-    loader = ContrastiveLoader(synthetic_dataset(4096, 10), a.batch, dev, seed=7)
+    loader = ContrastiveLoader(synthetic_dataset(max(2048, 4 * a.batch), 10, size=a.size), a.batch,
+                               dev, seed=7)
     it = iter(loader)
     for _ in range(2):  # warm-up + autotune
         tr.step(next(it)[0])
@@ -125,7 +130,8 @@ def main():
             parts[0] = parts[0].split(".")[0] + (".0" if parts[0].endswith(".0") else ".x")
         by_tag[" ".join(parts) or "(stem/head/loss/optim)"] += t
     tot = sum(v[1] for v in agg.values()) / a.steps
-    print(f"# per-op time, ResNet-50 CIFAR, batch {a.batch}x2 views, avg of {a.steps} steps\n")
+    print(f"# per-op time, {a.model} {'CIFAR' if a.cifar_stem else 'reference'} stem, {a.size}x{a.size}, "
+          f"batch {a.batch}x2 views, avg of {a.steps} steps\n")
     print(f"total timed op time/step: {tot / 1e3:.2f} ms\n")
     print("roofline per op: max(FLOP / 2.5 PF/s bf16 dense, compulsory bytes / 6.3 TB/s); "
           "% = roofline time / measured time; bound = which term dominates\n")
