@@ -916,6 +916,43 @@ void maxpool_bwd_op(const Tensor& dy, const Tensor& arg, const Tensor& dx, int64
               (int)S, (int)P, cur_stream());
 }
 
+// pooled ImageNet stem: BN + ReLU + max-pool forward, max-pool + ReLU-mask + BN backward
+void bn_relu_maxpool_op(const Tensor& a, const Tensor& ss, int64_t S, const Tensor& y,
+                        const Tensor& arg, const Tensor& asel, int64_t K, int64_t Sd, int64_t P) {
+  TORCH_CHECK(a.dim() == 4 && y.dim() == 4 && asel.dim() == 4, "bn_relu_maxpool: NHWC 4-D");
+  const int Nb = a.size(0), H = a.size(1), W = a.size(2), C = a.size(3);
+  const int OH = (H + 2 * P - K) / Sd + 1, OW = (W + 2 * P - K) / Sd + 1;
+  TORCH_CHECK(C % 8 == 0 && K >= 1 && K * K <= 255 && Sd >= 1 && P >= 0 && P < K,
+              "bn_relu_maxpool: geometry");
+  TORCH_CHECK(S >= 1 && Nb % S == 0, "bn_relu_maxpool: images must split evenly into views");
+  TORCH_CHECK(y.size(0) == Nb && y.size(1) == OH && y.size(2) == OW && y.size(3) == C &&
+                  asel.sizes() == y.sizes(), "bn_relu_maxpool: output shapes");
+  TORCH_CHECK(ss.numel() == 2 * S * C, "bn_relu_maxpool: scale/shift table [2][S][C]");
+  check_dev(arg, at::kByte, "arg");
+  TORCH_CHECK(arg.numel() == y.numel(), "bn_relu_maxpool: argmax size");
+  bn_relu_maxpool(bf(a, "a"), f32(ss, "ss"), (int)S, bfw(y, "y"), arg.data_ptr<uint8_t>(),
+                  bfw(asel, "asel"), Nb, H, W, C, OH, OW, (int)K, (int)Sd, (int)P, cur_stream());
+}
+
+void maxpool_bwd_bn_op(const Tensor& gy, const Tensor& arg, const Tensor& y, const Tensor& a,
+                       const Tensor& coef, int64_t S, const Tensor& da, int64_t K, int64_t Sd,
+                       int64_t P) {
+  TORCH_CHECK(a.dim() == 4 && da.dim() == 4 && gy.dim() == 4 && y.dim() == 4,
+              "maxpool_bwd_bn: NHWC 4-D");
+  const int Nb = a.size(0), H = a.size(1), W = a.size(2), C = a.size(3);
+  const int OH = (H + 2 * P - K) / Sd + 1, OW = (W + 2 * P - K) / Sd + 1;
+  TORCH_CHECK(C % 8 == 0 && K * K <= 255 && Sd >= 1 && P >= 0 && P < K, "maxpool_bwd_bn: geometry");
+  TORCH_CHECK(S >= 1 && Nb % S == 0, "maxpool_bwd_bn: images must split evenly into views");
+  TORCH_CHECK(gy.size(0) == Nb && gy.size(1) == OH && gy.size(2) == OW && gy.size(3) == C &&
+                  y.sizes() == gy.sizes() && da.sizes() == a.sizes(),
+              "maxpool_bwd_bn: shapes");
+  TORCH_CHECK(coef.numel() == 3 * S * C, "maxpool_bwd_bn: coef [3][S][C]");
+  check_dev(arg, at::kByte, "arg");
+  TORCH_CHECK(arg.numel() == gy.numel(), "maxpool_bwd_bn: argmax size");
+  maxpool_bwd_bn(bf(gy, "gy"), arg.data_ptr<uint8_t>(), bf(y, "y"), bf(a, "a"), f32(coef, "coef"),
+                 (int)S, bfw(da, "da"), Nb, H, W, C, OH, OW, (int)K, (int)Sd, (int)P, cur_stream());
+}
+
 void ce_topk_op(const Tensor& logits, const Tensor& y, double gscale, const Tensor& loss,
                 const Tensor& rank, const c10::optional<Tensor>& dlogits) {
   TORCH_CHECK(logits.dim() == 2, "ce_topk: logits [B][C]");
@@ -950,6 +987,10 @@ void class_sums_op(const Tensor& X, const Tensor& y, int64_t NC, const Tensor& s
 TORCH_LIBRARY(simclr_amd, m) {
   m.def("maxpool_fwd(Tensor x, Tensor(a!) y, Tensor(b!) arg, int K, int S, int P) -> ()", &maxpool_fwd_op);
   m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
+  m.def("bn_relu_maxpool(Tensor a, Tensor ss, int S, Tensor(a!) y, Tensor(b!) arg, Tensor(c!) asel, "
+        "int K, int Sd, int P) -> ()", &bn_relu_maxpool_op);
+  m.def("maxpool_bwd_bn(Tensor gy, Tensor arg, Tensor y, Tensor a, Tensor coef, int S, Tensor(a!) da, "
+        "int K, int Sd, int P) -> ()", &maxpool_bwd_bn_op);
   m.def("ce_topk(Tensor logits, Tensor y, float gscale, Tensor(a!) loss, Tensor(b!) rank, Tensor(c!)? dlogits=None) -> ()", &ce_topk_op);
   m.def("class_sums(Tensor X, Tensor y, int NC, Tensor(a!) sums, Tensor(b!) counts) -> ()", &class_sums_op);
   m.def("igemm(Tensor A, Tensor B, Tensor(a!) out, Tensor? bias, Tensor(b!)? stats, int[] geom, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int epi_mode=0, Tensor? epi_a=None, Tensor? epi_b=None, int variant=-1, Tensor? epi_ss=None, Tensor? epi_mi=None, int seg_rows=0, int stats_seg_blocks=0, int stats_base=0, Tensor? epi_c=None, Tensor? epi_mask=None, Tensor? epi_c2=None, Tensor? epi_mi2=None, Tensor(c!)? stats2=None, Tensor? pro_d=None, Tensor? A2=None, Tensor? pro_rss=None, Tensor(d!)? pro_out=None, Tensor(e!)? pro_mask=None) -> ()", &igemm);

@@ -101,6 +101,145 @@ __global__ void k_maxpool_bwd(const uint16_t* __restrict__ dy, const uint8_t* __
   }
 }
 
+// ---------------------------------------------------------------------------- pooled stem
+// The ImageNet-shape stem (reference model.py:90-92 keeps torchvision's 7x7/s2 conv -> BN ->
+// ReLU -> MaxPool2d(3, 2, 1) for resnet50), fused around the max-pool:
+//   forward   out = maxpool(relu(ss0[view]·a + ss1[view])) straight from the pre-BN conv output
+//             a: the full-resolution BN + ReLU output is never written (the unfused path writes
+//             it and reads it back).  Besides the window tap (one byte, for the backward) the
+//             kernel keeps the pre-BN value at the argmax (asel), so the BatchNorm backward
+//             partials Σg, Σg·x̂ come from pooled-size tensors (k_bn_bwd_reduce over out / asel:
+//             g is zero off the argmax positions, and relu'(y[argmax]) = [out > 0]);
+//   backward  da = A·g + B·a + D at full resolution, g gathered from the windows whose argmax
+//             is this position (ReLU mask [out > 0]): max-pool backward, ReLU mask and the
+//             BatchNorm input gradient in one pass (the unfused path scatters g, reduces over g
+//             and a, and applies: three full-resolution passes).
+// Values are compared after bf16 rounding, as the unfused BN-apply pass stores them; the first
+// maximum in window order wins (strict >), NaN wins, as in k_maxpool_fwd.
+__global__ void k_bn_relu_maxpool(const uint16_t* __restrict__ a, const float* __restrict__ ss,
+                                  int S, uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                  uint16_t* __restrict__ asel, int Nb, int H, int W, int C,
+                                  int OH, int OW, int K, int Sd, int P) {
+  const int CH = C / 8;
+  const int per_seg = Nb / S;
+  const size_t total = (size_t)Nb * OH * OW * CH;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CH);
+    const size_t pix = i / CH;
+    const int ow = (int)(pix % OW);
+    const int oh = (int)((pix / OW) % OH);
+    const int n = (int)(pix / ((size_t)OW * OH));
+    const int seg = n / per_seg;
+    float sc[8], sh[8], best[8];
+    int bt[8];
+    uint32_t ba[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = ss[seg * C + cc * 8 + e];
+      sh[e] = ss[S * C + seg * C + cc * 8 + e];
+      best[e] = -INFINITY;
+      bt[e] = 0;
+      ba[e] = 0;
+    }
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = oh * Sd - P + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int iw = ow * Sd - P + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const u32x4 v = *(const u32x4*)(a + (((size_t)n * H + ih) * W + iw) * C + cc * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t w = v[e >> 1];
+          const float av = (e & 1) ? hi_bf(w) : lo_bf(w);
+          float f = fmaf(av, sc[e], sh[e]);
+          f = f > 0.f ? f : (f != f ? f : 0.f);
+          f = bf2f(f2bf(f));
+          if (f > best[e] || f != f) {
+            best[e] = f;
+            bt[e] = kh * K + kw;
+            ba[e] = (e & 1) ? (w >> 16) : (w & 0xffffu);
+          }
+        }
+      }
+    }
+    u32x4 wy, wa;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      wy[e] = pack2bf(best[2 * e], best[2 * e + 1]);
+      wa[e] = ba[2 * e] | (ba[2 * e + 1] << 16);
+    }
+    *(u32x4*)(y + pix * C + cc * 8) = wy;
+    *(u32x4*)(asel + pix * C + cc * 8) = wa;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a0 |= (uint32_t)bt[e] << (8 * e);
+      a1 |= (uint32_t)bt[e + 4] << (8 * e);
+    }
+    *(u32x2*)(arg + pix * C + cc * 8) = (u32x2){a0, a1};
+  }
+}
+
+// da[n][ih][iw][c] = A·g + B·a + D, g = Σ over the windows containing (ih, iw) whose argmax is
+// this tap and whose pooled output is positive (the ReLU mask) of the pooled gradient
+__global__ void k_maxpool_bwd_bn(const uint16_t* __restrict__ gy, const uint8_t* __restrict__ arg,
+                                 const uint16_t* __restrict__ y, const uint16_t* __restrict__ a,
+                                 const float* __restrict__ coef, int S, uint16_t* __restrict__ da,
+                                 int Nb, int H, int W, int C, int OH, int OW, int K, int Sd,
+                                 int P) {
+  const int CH = C / 8;
+  const int per_seg = Nb / S;
+  const size_t total = (size_t)Nb * H * W * CH;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CH);
+    const size_t pix = i / CH;
+    const int iw = (int)(pix % W);
+    const int ih = (int)((pix / W) % H);
+    const int n = (int)(pix / ((size_t)W * H));
+    const int seg = n / per_seg;
+    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int oh0 = max(0, (ih + P - K + Sd) / Sd), oh1 = min(OH - 1, (ih + P) / Sd);
+    const int ow0 = max(0, (iw + P - K + Sd) / Sd), ow1 = min(OW - 1, (iw + P) / Sd);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const int kh = ih - (oh * Sd - P);
+      if (kh < 0 || kh >= K) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int kw = iw - (ow * Sd - P);
+        if (kw < 0 || kw >= K) continue;
+        const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + cc * 8;
+        const u32x2 t8 = *(const u32x2*)(arg + o);
+        const u32x4 v = *(const u32x4*)(gy + o);
+        const u32x4 yv = *(const u32x4*)(y + o);
+        const int tap = kh * K + kw;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int t = (int)(((e < 4 ? t8[0] : t8[1]) >> (8 * (e & 3))) & 0xffu);
+          const float yy = (e & 1) ? hi_bf(yv[e >> 1]) : lo_bf(yv[e >> 1]);
+          if (t == tap && yy > 0.f) g[e] += (e & 1) ? hi_bf(v[e >> 1]) : lo_bf(v[e >> 1]);
+        }
+      }
+    }
+    const u32x4 av = *(const u32x4*)(a + pix * C + cc * 8);
+    u32x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float r[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = 2 * e + h;
+        const int c = seg * C + cc * 8 + k;
+        const float x = h ? hi_bf(av[e]) : lo_bf(av[e]);
+        r[h] = coef[c] * g[k] + coef[S * C + c] * x + coef[2 * S * C + c];
+      }
+      w[e] = pack2bf(r[0], r[1]);
+    }
+    *(u32x4*)(da + pix * C + cc * 8) = w;
+  }
+}
+
 // ---------------------------------------------------------------------------- CE + top-k
 // logits [B][C] fp32, y [B] int64.  Per row: loss = lse - logit[y]; rank = #{j: logit[j] >
 // logit[y]} + #{j < y: logit[j] == logit[y]} + #{j != y: logit[j] is NaN} (torch.topk orders NaN
@@ -211,6 +350,22 @@ void maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int Nb, i
                  int C, int OH, int OW, int K, int S, int P, hipStream_t s) {
   hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_cap((size_t)Nb * H * W * (C / 8))), dim3(256), 0, s,
                      dy, arg, dx, Nb, H, W, C, OH, OW, K, S, P);
+  HIP_CHECK_LAUNCH();
+}
+
+void bn_relu_maxpool(const uint16_t* a, const float* ss, int S, uint16_t* y, uint8_t* arg,
+                     uint16_t* asel, int Nb, int H, int W, int C, int OH, int OW, int K, int Sd,
+                     int P, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_relu_maxpool, dim3(grid_cap((size_t)Nb * OH * OW * (C / 8))), dim3(256),
+                     0, s, a, ss, S, y, arg, asel, Nb, H, W, C, OH, OW, K, Sd, P);
+  HIP_CHECK_LAUNCH();
+}
+
+void maxpool_bwd_bn(const uint16_t* gy, const uint8_t* arg, const uint16_t* y, const uint16_t* a,
+                    const float* coef, int S, uint16_t* da, int Nb, int H, int W, int C, int OH,
+                    int OW, int K, int Sd, int P, hipStream_t s) {
+  hipLaunchKernelGGL(k_maxpool_bwd_bn, dim3(grid_cap((size_t)Nb * H * W * (C / 8))), dim3(256), 0,
+                     s, gy, arg, y, a, coef, S, da, Nb, H, W, C, OH, OW, K, Sd, P);
   HIP_CHECK_LAUNCH();
 }
 

@@ -232,6 +232,12 @@ void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int Nb, int H, in
                  int OH, int OW, int K, int S, int P, hipStream_t s);
 void maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int Nb, int H, int W,
                  int C, int OH, int OW, int K, int S, int P, hipStream_t s);
+void bn_relu_maxpool(const uint16_t* a, const float* ss, int S, uint16_t* y, uint8_t* arg,
+                     uint16_t* asel, int Nb, int H, int W, int C, int OH, int OW, int K, int Sd,
+                     int P, hipStream_t s);
+void maxpool_bwd_bn(const uint16_t* gy, const uint8_t* arg, const uint16_t* y, const uint16_t* a,
+                    const float* coef, int S, uint16_t* da, int Nb, int H, int W, int C, int OH,
+                    int OW, int K, int Sd, int P, hipStream_t s);
 void ce_topk(const float* logits, const int64_t* y, int B, int C, float gscale, float* loss,
              int* rank, float* dlogits, hipStream_t s);
 size_t class_sums_lds(int NC);

@@ -124,6 +124,8 @@ class _BlockTape:
     bnd: Optional[_BNState] = None
     out: Optional[torch.Tensor] = None
     mask: Optional[torch.Tensor] = None  # uint8 ReLU bitmask of ``out`` (bit per channel)
+    # pooled stem only: (window argmax bytes, pre-BN value at the argmax) of the max-pool
+    pool: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
 
 # persistent blocks per view segment of the fused 1x1 backward (2 segments: 2x this many blocks)
@@ -208,14 +210,21 @@ class FusedStages:
         self.stem_fused = type(self).STEM_FUSED
         self.stem = None
         self._stem_block = None
+        # the ImageNet stem's max-pool (k, stride, pad), fused around (stem_forward / backward):
+        # BN + ReLU + max-pool in one pass, the max-pool / ReLU / BN backward in one pass
+        self.stem_pool = None
         from .resnet import _Identity
-        if isinstance(getattr(resnet, "maxpool", None), _Identity):
+        from ..ops.pooling import MaxPool2d
+        mp = getattr(resnet, "maxpool", None)
+        if isinstance(mp, (_Identity, MaxPool2d)):
             c1 = resnet.conv1
             k = c1.kernel_size[0] if isinstance(c1.kernel_size, tuple) else c1.kernel_size
             st_ = c1.stride[0] if isinstance(c1.stride, tuple) else c1.stride
             pd = c1.padding[0] if isinstance(c1.padding, tuple) else c1.padding
             self.stem = _ConvSpec(c1, resnet.bn1, st_, k, pd)
             self._stem_block = _BlockSpec([self.stem], None, "stem")
+            if isinstance(mp, MaxPool2d):
+                self.stem_pool = (int(mp.kernel_size), int(mp.stride), int(mp.padding))
         self.blocks: List[_BlockSpec] = []
         for li, layer in enumerate((resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4)):
             for bi, blk in enumerate(layer):
@@ -254,6 +263,14 @@ class FusedStages:
         cs = self.stem
         OH = (H + 2 * cs.pad - cs.k) // cs.stride + 1
         OW = (W + 2 * cs.pad - cs.k) // cs.stride + 1
+        if self.stem_pool is not None:
+            # the stem weight gradient reads a materialised BN input gradient (no 256-row
+            # BN-backward prologue splits); the blocks see the pooled map
+            K, Sd, P = self.stem_pool
+            if Nb % self.S or ((Nb // self.S) * OH * OW) % 64 or self.stem.conv.out_channels % 8:
+                return False
+            PH, PW = (OH + 2 * P - K) // Sd + 1, (OW + 2 * P - K) // Sd + 1
+            return self._shape_ok(Nb, PH, PW)
         if Nb % self.S or ((Nb // self.S) * OH * OW) % 256:
             return False
         return self._shape_ok(Nb, OH, OW)
@@ -859,10 +876,22 @@ class FusedStages:
         cs = self.stem
         _ext.TAG = "stem fwd"
         a, bs = self._conv_bn_fwd(ops, img, cs, None, S, st)
-        x0 = torch.empty_like(a)
-        mask = torch.empty((a.numel() // 8,), device=a.device, dtype=torch.uint8)
-        ops.bn_apply_ss(a, bs.ss, None, None, x0, S, True, mask)
-        tp = _BlockTape(x=img, acts=[a], bns=[bs], out=x0, mask=mask)
+        if self.stem_pool is not None:
+            # maxpool(relu(bn(a))) in one pass; the full-resolution BN output is never written
+            K, Sd, P = self.stem_pool
+            Nb, OH, OW, C = a.shape
+            PH, PW = (OH + 2 * P - K) // Sd + 1, (OW + 2 * P - K) // Sd + 1
+            x0 = _empty_nhwc(Nb, PH, PW, C, a.device)
+            arg = torch.empty(x0.shape, device=a.device, dtype=torch.uint8)
+            asel = torch.empty_like(x0)
+            _ext.TAG = "stem bn+relu+maxpool"
+            ops.bn_relu_maxpool(a, bs.ss.view(-1), S, x0, arg, asel, K, Sd, P)
+            tp = _BlockTape(x=img, acts=[a], bns=[bs], out=x0, pool=(arg, asel))
+        else:
+            x0 = torch.empty_like(a)
+            mask = torch.empty((a.numel() // 8,), device=a.device, dtype=torch.uint8)
+            ops.bn_apply_ss(a, bs.ss, None, None, x0, S, True, mask)
+            tp = _BlockTape(x=img, acts=[a], bns=[bs], out=x0, mask=mask)
         out, tapes = self.forward(x0)
         return out, tapes, tp
 
@@ -904,7 +933,11 @@ class FusedStages:
             if store is not None:
                 store.producer_streams = [main, self._side]
         g, pre = gout, None
-        stem_prev = (self._stem_block, stem_tape) if stem_tape is not None else None
+        pooled = stem_tape is not None and stem_tape.pool is not None
+        # a pooled stem is not a block-boundary producer (the max-pool sits between its BN and
+        # layer1.0): layer1.0 returns the raw gradient of the pooled map
+        stem_prev = (self._stem_block, stem_tape) if (stem_tape is not None and not pooled) \
+            else None
         hook = getattr(self.resnet, "stage_grads_ready", None) if main is not None else None
         for idx in range(len(self.blocks) - 1, -1, -1):
             prev = (self.blocks[idx - 1], tapes[idx - 1]) if idx > 0 else stem_prev
@@ -918,7 +951,26 @@ class FusedStages:
                 self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):
                     hook(stage)
-        if stem_tape is not None:
+        if pooled:
+            # g = dL/d(pooled map).  BatchNorm partials from pooled-size tensors (g is zero off
+            # the window argmaxes; relu'(y[argmax]) = [pooled > 0]), then ONE full-resolution
+            # pass: max-pool backward + ReLU mask + BN input gradient (k_maxpool_bwd_bn)
+            _ext.TAG = "stem bwd"
+            arg, asel = stem_tape.pool
+            a0, bs0, x0 = stem_tape.acts[0], stem_tape.bns[0], stem_tape.out
+            C = a0.shape[-1]
+            nblk = ops.bn_blocks(x0.numel() // C, C, S)
+            partial = torch.empty((S * nblk * 2 * C,), device=a0.device, dtype=torch.float32)
+            ops.bn_bwd_reduce(g, x0, asel, bs0.mi, S, True, partial)
+            coef = self._bn_bwd(ops, self.stem.bn, partial, nblk, bs0, S, st)
+            da = torch.empty_like(a0)
+            K, Sd, P = self.stem_pool
+            ops.maxpool_bwd_bn(g, arg, x0, a0, coef, S, da, K, Sd, P)
+            _ext.TAG = "stem wgrad"
+            self._wgrad(ops, da, stem_tape.x, self.stem, None, S, main=True)
+            _ext.TAG = ""
+            g = None
+        elif stem_tape is not None:
             # g = dL/d(stem output)·[y > 0] with the stem BatchNorm's partials from layer1.0's
             # conv1 dgrad epilogue: finish its backward, weight gradient with the BN backward in
             # the dY prologue (da never materialised)

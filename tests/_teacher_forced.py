@@ -42,7 +42,7 @@ import torch.nn.functional as F
 # 6.3e-8, the stored prologue operand 1.1e-5).  A 0.2 % weight-gradient defect is 20x over its
 # bound.
 BOUNDS = {"y": 4e-3, "bnfwd": 1e-5, "out": 4e-3, "mask": 1e-6, "dx": 5e-3, "dy_op": 1e-4,
-          "dW": 1e-4, "dgb": 1e-5, "bnbwd": 1e-5}
+          "dW": 1e-4, "dgb": 1e-5, "bnbwd": 1e-5, "pool_tie": 1e-3}
 
 
 def _nchw(t: torch.Tensor) -> torch.Tensor:
@@ -83,6 +83,7 @@ class Recorder:
         self.tapes = []
         self.stem_tape = None
         self.stem_cs = None
+        self.stem_pool = None
         self.blocks = None
         self.dgrads: List[dict] = []
         self.wgrads: List[dict] = []
@@ -109,6 +110,7 @@ class Recorder:
             out, tapes, tp = orig["stem_forward"](self_, img)
             rec.stem_tape = tp
             rec.stem_cs = self_.stem
+            rec.stem_pool = self_.stem_pool
             return out, tapes, tp
 
         def bn_fwd(self_, ops, bn, *a, **kw):
@@ -270,9 +272,54 @@ class Recorder:
             seg = _seg_rows(a, S)
             ss = bs.ss.view(2, S * C)
             ref = torch.relu(a.float() * _per_seg(ss[0], seg, S, C) + _per_seg(ss[1], seg, S, C))
-            self._err("out", "stem", tp.out, ref)
-            bits = _mask_bits(tp.mask, tp.out.numel())
-            self._err("mask", "stem", bits.float(), (tp.out.reshape(-1).float() > 0).float())
+            if tp.pool is not None:
+                # fused BN + ReLU + max-pool: pooled values, and the recorded argmax / pre-BN
+                # value point at a window element that holds that maximum
+                K, Sd, P = self.stem_pool
+                pref = F.max_pool2d(_nchw_f(_bf(ref)), K, Sd, P).permute(0, 2, 3, 1)
+                self._err("out", "stem (pooled)", tp.out, pref)
+                arg, asel = tp.pool
+                ih, iw = self._argmax_pos(arg, tp.out.shape, a.shape)
+                n_ = torch.arange(a.shape[0], device=a.device)[:, None, None, None]
+                c_ = torch.arange(C, device=a.device)[None, None, None, :]
+                picked = a[n_, ih, iw, c_]
+                self.errors["mask"].append(
+                    ("stem argmax value", float((asel != picked).float().mean())))
+                # (torch's a·sc + sh vs the kernel's fma can differ in the last fp32 bit and flip
+                # a bf16 rounding: ~1e-4 of the elements, measured 8.2e-5)
+                yv = _bf(ref)[n_, ih, iw, c_]
+                self.errors["pool_tie"].append(
+                    ("stem argmax is max", float((yv != tp.out.float()).float().mean())))
+            else:
+                self._err("out", "stem", tp.out, ref)
+                bits = _mask_bits(tp.mask, tp.out.numel())
+                self._err("mask", "stem", bits.float(), (tp.out.reshape(-1).float() > 0).float())
+
+    def _argmax_pos(self, arg, pshape, fshape):
+        """Full-resolution (ih, iw) of every pooled element's window argmax, [N, PH, PW, C]."""
+        K, Sd, P = self.stem_pool
+        N, PH, PW, C = pshape
+        t = arg.long()
+        oh = torch.arange(PH, device=arg.device)[None, :, None, None]
+        ow = torch.arange(PW, device=arg.device)[None, None, :, None]
+        return oh * Sd - P + t // K, ow * Sd - P + t % K
+
+    def _pooled_stem_g(self):
+        """The stem BatchNorm's full-resolution g from the pooled gradient (layer1.0's raw input
+        gradient, recorded), scattered to the recorded window argmaxes, ReLU-masked."""
+        tp = self.stem_tape
+        gp = next(r["out"] for r in self.dgrads if self.names.get(id(r["cs"].conv)) ==
+                  "layer1.0.conv1")
+        a = tp.acts[0]
+        N, H, W, C = a.shape
+        arg, _ = tp.pool
+        ih, iw = self._argmax_pos(arg, tp.out.shape, a.shape)
+        val = gp.float() * (tp.out.float() > 0)
+        flat = ((torch.arange(N, device=a.device)[:, None, None, None] * H + ih) * W + iw) * C + \
+            torch.arange(C, device=a.device)[None, None, None, :]
+        g = torch.zeros(N * H * W * C, device=a.device)
+        g.index_add_(0, flat.reshape(-1), val.reshape(-1))
+        return g.view(N, H, W, C)
 
     def check_dgrads(self):
         S = self.S
@@ -345,6 +392,20 @@ class Recorder:
             if b.down is not None:
                 acts[id(b.down.bn)] = (tp.ad, tp.bnd)
         coef_of = {id(c["bn"]): c["coef"] for c in self.coefs}
+        if self.stem_tape is not None and self.stem_tape.pool is not None:
+            self.bn_g[id(self.stem_cs.bn)] = self._pooled_stem_g()
+            coef = coef_of.get(id(self.stem_cs.bn))
+            w = next((r for r in self.wgrads if r["cs"] is self.stem_cs), None)
+            if coef is not None and w is not None:
+                # the max-pool / ReLU / BN backward pass output (the stem weight gradient's dY)
+                a = self.stem_tape.acts[0]
+                g = self.bn_g[id(self.stem_cs.bn)]
+                C = a.shape[-1]
+                seg = _seg_rows(a, S)
+                A, B, D = coef[:S * C], coef[S * C:2 * S * C], coef[2 * S * C:]
+                ref = (_per_seg(A, seg, S, C) * g + _per_seg(B, seg, S, C) * a.float()
+                       + _per_seg(D, seg, S, C))
+                self._err("dx", "stem maxpool+bn bwd", w["dyn"], ref)
         mods = {id(m): m for m in self.bn_of.values()}
         for key, g in self.bn_g.items():
             bn = mods.get(key)

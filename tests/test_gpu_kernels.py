@@ -616,3 +616,67 @@ def test_wgrad_bn_backward_prologue_padded_channels(ops, k, s, p, H):
     run_wgrad(ops, dyn, xn, out, g, Creal, dpro=(Yn, coef, seg, S))
     assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2
     assert checked >= len(vs)
+
+
+@pytest.mark.parametrize("N,H,C", [(4, 16, 64), (6, 17, 64), (2, 112, 64)])
+def test_pooled_stem_kernels(ops, N, H, C):
+    """The ImageNet stem's fused BN + ReLU + MaxPool2d(3, 2, 1) forward (bn_relu_maxpool) and
+    max-pool / ReLU-mask / BN input-gradient backward (maxpool_bwd_bn) against fp32 torch on the
+    same bf16 operands: pooled values, the recorded argmax / pre-BN value, and
+    da = A·g + B·a + D with g = max-pool backward of the pooled gradient masked by [pooled > 0]
+    (odd H: windows clipped at the border)."""
+    torch.manual_seed(N * H + C)
+    S, K, Sd, P = 2, 3, 2, 1
+    a = _bf(torch.randn(N, H, H, C, device=DEV))
+    ss = torch.cat([torch.rand(S, C, device=DEV) + 0.5,
+                    torch.randn(S, C, device=DEV) * 0.5]).reshape(-1).contiguous()
+    OH = (H + 2 * P - K) // Sd + 1
+    y = torch.empty(N, OH, OH, C, device=DEV, dtype=torch.bfloat16)
+    arg = torch.empty(y.shape, device=DEV, dtype=torch.uint8)
+    asel = torch.empty_like(y)
+    ops.bn_relu_maxpool(a, ss, S, y, arg, asel, K, Sd, P)
+    seg = torch.arange(N, device=DEV) // (N // S)
+    sc = ss[:S * C].view(S, C)[seg][:, None, None, :]
+    sh = ss[S * C:].view(S, C)[seg][:, None, None, :]
+    r = _bf(torch.relu(torch.addcmul(sh, a.float(), sc))).float()  # what a BN-apply pass stores
+    ref, idx = F.max_pool2d(r.permute(0, 3, 1, 2), K, Sd, P, return_indices=True)
+    # (torch may round the affine differently from the kernel's fma in the last fp32 bit,
+    # which can flip a bf16 rounding now and then)
+    assert (y.float() != ref.permute(0, 2, 3, 1)).float().mean().item() < 1e-3
+    assert _rel(y, ref.permute(0, 2, 3, 1)) < 1e-2
+    # the recorded tap points at a window element holding the maximum, and asel is its a
+    t = arg.long()
+    ih = torch.arange(OH, device=DEV)[None, :, None, None] * Sd - P + t // K
+    iw = torch.arange(OH, device=DEV)[None, None, :, None] * Sd - P + t % K
+    n_ = torch.arange(N, device=DEV)[:, None, None, None]
+    c_ = torch.arange(C, device=DEV)[None, None, None, :]
+    assert (r[n_, ih, iw, c_] != y.float()).float().mean().item() < 1e-3
+    assert torch.equal(a[n_, ih, iw, c_], asel)
+    # backward
+    gy = _bf(torch.randn_like(y.float()))
+    coef = torch.cat([torch.rand(S, C, device=DEV) + 0.5, torch.randn(S, C, device=DEV) * 0.2,
+                      torch.randn(S, C, device=DEV) * 0.1]).reshape(-1).contiguous()
+    da = torch.empty_like(a)
+    ops.maxpool_bwd_bn(gy, arg, y, a, coef, S, da, K, Sd, P)
+    flat = ((n_ * H + ih) * H + iw) * C + c_
+    g = torch.zeros(N * H * H * C, device=DEV)
+    g.index_add_(0, flat.reshape(-1), (gy.float() * (y.float() > 0)).reshape(-1))
+    g = g.view(N, H, H, C)
+    A = coef[:S * C].view(S, C)[seg][:, None, None, :]
+    B = coef[S * C:2 * S * C].view(S, C)[seg][:, None, None, :]
+    D = coef[2 * S * C:].view(S, C)[seg][:, None, None, :]
+    dref = A * g + B * a.float() + D
+    assert _rel(da, dref) < 1e-2
+    # the BatchNorm-backward partials from pooled-size tensors equal the full-resolution sums
+    mi = torch.cat([torch.randn(S, C, device=DEV) * 0.1,
+                    torch.rand(S, C, device=DEV) + 0.5]).reshape(-1).contiguous()
+    nblk = ops.bn_blocks(y.numel() // C, C, S)
+    part = torch.empty(S * nblk * 2 * C, device=DEV)
+    ops.bn_bwd_reduce(gy, y, asel, mi, S, True, part)
+    sums = part.view(S, nblk, 2, C).sum(1)
+    xh = (a.float() - mi[:S * C].view(S, C)[seg][:, None, None, :]) * \
+        mi[S * C:].view(S, C)[seg][:, None, None, :]
+    for s_ in range(S):
+        gs = g[seg == s_].reshape(-1, C)
+        assert _rel(sums[s_, 0], gs.sum(0)) < 1e-3
+        assert _rel(sums[s_, 1], (gs * xh[seg == s_].reshape(-1, C)).sum(0)) < 1e-3

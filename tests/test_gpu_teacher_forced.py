@@ -18,8 +18,10 @@ def _report(tag, errors):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("base,stem", [("resnet50", True), ("resnet18", None)])
+@pytest.mark.parametrize("base,stem", [("resnet50", True), ("resnet18", None), ("resnet50", None)])
 def test_teacher_forced_every_op_batch512(base, stem, monkeypatch):
+    """(resnet50, None) is the reference's ResNet-50 (ImageNet 7x7/s2 stem + max-pool on 32x32):
+    its stem runs as the fused BN + ReLU + max-pool forward and max-pool / ReLU / BN backward."""
     from _teacher_forced import BOUNDS, run_step, violations
     errors, counts, rec = run_step(base, stem, 512, monkeypatch)
     _report(base, errors)
@@ -34,7 +36,10 @@ def test_teacher_forced_every_op_batch512(base, stem, monkeypatch):
     assert counts["bnfwd"] == 2 * nconv, counts
     assert counts["dgb"] == 2 * nconv, counts
     assert counts["bnbwd"] >= nconv - 1, counts
-    assert counts["out"] == len(rec.blocks) + 1 and counts["mask"] == counts["out"], counts
+    pooled = rec.stem_tape is not None and rec.stem_tape.pool is not None
+    assert pooled == (stem is None and base == "resnet50"), "pooled stem not fused"
+    assert counts["out"] == len(rec.blocks) + 1, counts
+    assert counts["mask"] == counts["out"], counts
     if base == "resnet50":
         assert nconv == 53
 
