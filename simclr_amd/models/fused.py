@@ -207,6 +207,13 @@ class FusedStages:
         # boundary) and its weight gradient applies the BN backward in the dY prologue — no
         # separate reduce pass over the 1024 x 32 x 32 x 64 stem activation, no materialised
         # input gradient (stem_forward / backward)
+        # A/B of the fusion switches above without code edits (tools/envab.sh):
+        # SIMCLR_FUSED_ATTRS="attr=value,..." (ints / true / false), applied at construction
+        for kv in filter(None, os.environ.get("SIMCLR_FUSED_ATTRS", "").split(",")):
+            k, v = kv.split("=", 1)
+            if not hasattr(self, k):
+                raise ValueError(f"SIMCLR_FUSED_ATTRS: FusedStages has no switch {k!r}")
+            setattr(self, k, v.lower() == "true" if v.lower() in ("true", "false") else int(v))
         self.stem_fused = type(self).STEM_FUSED
         self.stem = None
         self._stem_block = None
