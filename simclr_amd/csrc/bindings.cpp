@@ -352,11 +352,16 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
 void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
                          const c10::optional<Tensor>& coef, const Tensor& X, const Tensor& xss,
                          const Tensor& xmi, const Tensor& Wt, const Tensor& gm,
-                         const Tensor& stats, const Tensor& wpart, int64_t S, int64_t bps) {
+                         const Tensor& stats, const Tensor& wpart, int64_t S, int64_t bps,
+                         const c10::optional<Tensor>& Xraw) {
   const int64_t CI = gm.size(-1);
   const int64_t M = gm.numel() / CI;
   const int64_t CO = G.numel() / M;
-  TORCH_CHECK(CO == 256 && CI == 64, "conv1x1_bwd_dual: Co = 256, Ci = 64 only");
+  const uint16_t* xr = optbf(Xraw, "Xraw");
+  TORCH_CHECK((CO == 256 && CI == 64 && xr == nullptr) || (CO == 512 && CI == 128),
+              "conv1x1_bwd_dual: (Co, Ci) = (256, 64) or (512, 128); a pre-applied X (Xraw "
+              "given) only with (512, 128)");
+  if (xr != nullptr) TORCH_CHECK(Xraw->numel() == M * CI, "conv1x1_bwd_dual: Xraw size");
   TORCH_CHECK(G.numel() == M * CO && X.numel() == M * CI && Wt.numel() == CI * CO,
               "conv1x1_bwd_dual: operand sizes");
   TORCH_CHECK(S >= 1 && S <= 2 && bps >= 1 && M % S == 0 && (M / S) % (64 * bps) == 0,
@@ -373,7 +378,7 @@ void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
   }
   conv1x1_bwd_dual(bf(G, "G"), a3, cf, bf(X, "X"), f32(xss, "xss"), f32(xmi, "xmi"),
                    bf(Wt, "Wt"), bfw(gm, "gm"), f32w(stats, "stats"), f32w(wpart, "wpart"),
-                   (int)M, (int)CO, (int)CI, (int)S, (int)bps, cur_stream());
+                   (int)M, (int)CO, (int)CI, (int)S, (int)bps, cur_stream(), xr);
 }
 
 void wgrad_reduce_slabs_op(const Tensor& partial, int64_t splits, const Tensor& out, double beta) {
@@ -1014,7 +1019,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("wgrad_variant_ok(int v, int[] geom, bool pro, bool dy_pro) -> bool", &wgrad_vok);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad_tiles(int[] geom, int variant=-1) -> int", &wgrad_ntiles);
-  m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor xss, Tensor xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps) -> ()", &conv1x1_bwd_dual_op);
+  m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor xss, Tensor xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps, Tensor? Xraw=None) -> ()", &conv1x1_bwd_dual_op);
   m.def("wgrad_reduce_slabs(Tensor(a!) partial, int splits, Tensor(b!) out, float beta=0.0) -> ()", &wgrad_reduce_slabs_op);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);

@@ -2855,6 +2855,10 @@ struct Dual1x1Args {
   float* wpart;          // [S * bps][CO][CI] dW slabs
   int M, S, seg_rows, bps, tiles_per_block;
   uint32_t g_bytes, x_bytes;
+  // wide form only: X already holds relu(bn2(a2)) (the forward materialised it), Xraw = a2 for
+  // the epilogue's mask / x̂
+  const uint16_t* Xraw;
+  int x_pre;
 };
 
 template <int CO, int CI>
@@ -3067,6 +3071,207 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
     }
     p.stats[((size_t)blk * 2 + 0) * CI + tid] = a;
     p.stats[((size_t)blk * 2 + 1) * CI + tid] = b;
+  }
+}
+
+// Wide form of the fused 1x1 backward for Co = 512, Ci = 128 (ResNet-50 layer2 conv3, whose
+// backward otherwise reads its 2 x 268 MB BN3-backward operands twice: the dgrad on the chain,
+// the weight gradient again on the side stream).  Wᵀ [128][512] alone would fill 128 KB of LDS,
+// so a block owns one 64-channel slice of Ci (its Wᵀ slice, 64 KB, resident) and the CIT / 64
+// slices of a row range are consecutive logical blocks: xcd_remap puts them on one XCD, so the
+// second read of each dY tile is an L2 hit.  32-row m-tiles, 8 waves (the 4-wave form of the
+// narrow kernel spilled at this width), two register sets and two LDS buffers: two tiles
+// (144 KB with the lazy BN3 operand) in flight per CU.  Per tile, wave w:
+//   dX[16 rows (w & 1) x 16 ci (w >> 1)] = dY · W-slice  (mode-3 epilogue: BN2 mask, partials)
+//   dW[64 co (w) x 64 ci] += dYᵀ · X-slice
+// X is either a2 with BN2 + ReLU applied while staging (XPRE = false) or the forward's
+// materialised relu(bn2(a2)) (XPRE, a2 read beside it for the epilogue).  The per-channel
+// tables live in LDS (registers are the constraint here).
+template <int CO, int CIT, bool LAZY, bool XPRE>
+__global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
+  constexpr int CI = 64;   // channels of Ci per block
+  constexpr int NH = CIT / CI;
+  constexpr int BMT = 32;  // rows per m-tile
+  constexpr int NT = 512;
+  static_assert(CO == 512 && CIT % CI == 0, "wide dual tile mapping (64 output channels per wave)");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Ds = (uint16_t*)smem;          // [2][32][CO]  tr_swz<CO> image of dY
+  uint16_t* Xs = Ds + 2 * BMT * CO;        // [2][32][CI]  tr_swz<CI> image of relu(bn2(a2)) (slice)
+  uint16_t* Xr = Xs + 2 * BMT * CI;        // [2][32][CI]  raw a2 (slice)
+  uint16_t* Ws = Xr + 2 * BMT * CI;        // [CI][CO]     Wᵀ slice, chunk ^= row & 7
+  float* red = (float*)(Ws + CI * CO);     // [2 row halves][CI][2]
+  float* Tb = red + 2 * CI * 2;            // [4][CI]  BN2 scale, shift, mean, invstd (slice)
+  float* Cf = Tb + 4 * CI;                 // [3][CO]  BN3-backward A, B, D (LAZY)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar) selects
+  const int g = lane >> 4, li = lane & 15;
+  const int rh = wid & 1, cq = wid >> 1;   // dgrad: row half, 16-channel quarter of the slice
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int half = lb % NH;
+  const int blk = lb / NH;
+  const int c0 = half * CI;
+  const int seg = blk / p.bps;
+  const int mbeg = seg * p.seg_rows + (blk - seg * p.bps) * p.tiles_per_block * BMT;
+  const int T = p.tiles_per_block;
+
+  const __amdgpu_buffer_rsrc_t rg =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.G, (short)0, (int)p.g_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(LAZY ? p.A3 : p.G), (short)0, (int)p.g_bytes, 0x00020000);
+  // XPRE: threads 256.. load the raw a2 chunk the thread 256 below loads the transformed one of
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((XPRE && wid >= 4) ? p.Xraw : p.X), (short)0, (int)p.x_bytes, 0x00020000);
+
+  for (int c = tid; c < CI * CO / 8; c += NT) {
+    const int row = c / (CO / 8), ch = c % (CO / 8);
+    *(u32x4*)(Ws + row * CO + ((ch ^ (row & 7)) * 8)) =
+        *(const u32x4*)(p.Wt + ((size_t)(c0 + row) * CO + ch * 8));
+  }
+  for (int i = tid; i < 4 * CI; i += NT) {
+    const int k = i / CI, c = i % CI;
+    Tb[i] = (k < 2 ? p.xss : p.xmi)[((k & 1) * p.S + seg) * CIT + c0 + c];
+  }
+  if (LAZY)
+    for (int i = tid; i < 3 * CO; i += NT) {
+      const int k = i / CO, c = i % CO;
+      Cf[i] = p.coef[(k * p.S + seg) * CO + c];
+    }
+  constexpr int GCH = CO / 8, XCH = CI / 8;
+  constexpr int GR = NT / GCH;         // dY rows per loader pass
+  constexpr int GJ = BMT / GR;         // passes per tile
+  static_assert(256 / XCH == BMT, "one X chunk per thread (of the first 256) per tile");
+  const int gch = tid % GCH, grow = tid / GCH;
+  const int xt = tid & 255, xch = xt % XCH, xrow = xt / XCH;
+  const bool xload = XPRE || wid < 4;
+
+  u32x4 rG[2][GJ], rA[2][GJ], rX[2];
+  auto gload = [&](int t, u32x4 (&G8)[GJ], u32x4 (&A8)[GJ], u32x4& X1) {
+    const int m0 = mbeg + t * BMT;
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) {
+      const uint32_t off = (uint32_t)(((size_t)(m0 + grow + GR * j) * CO + gch * 8) * 2);
+      G8[j] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
+      if (LAZY) A8[j] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+    }
+    if (xload)
+      X1 = __builtin_amdgcn_raw_buffer_load_b128(
+          rx, (uint32_t)(((size_t)(m0 + xrow) * CIT + c0 + xch * 8) * 2), 0, 0);
+  };
+  auto lstore = [&](int buf, const u32x4 (&G8)[GJ], const u32x4 (&A8)[GJ], const u32x4& X1) {
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) {
+      const int r = grow + GR * j;
+      u32x4 v = G8[j];
+      if (LAZY) v = bnbwd8(G8[j], A8[j], Cf + gch * 8, Cf + CO + gch * 8, Cf + 2 * CO + gch * 8,
+                           true);
+      *(u32x4*)(Ds + buf * BMT * CO + r * CO + tr_swz<CO>(r, gch * 8)) = v;
+    }
+    if (wid < 4) {
+      *(u32x4*)(Xs + buf * BMT * CI + xrow * CI + tr_swz<CI>(xrow, xch * 8)) =
+          XPRE ? X1 : affine_relu8(X1, Tb + xch * 8, Tb + CI + xch * 8, true, true);
+      if (!XPRE) *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
+    } else if (XPRE) {
+      *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
+    }
+  };
+
+  f32x4 accw[CO / 8 / 16][CI / 16];
+#pragma unroll
+  for (int i = 0; i < CO / 8 / 16; ++i)
+#pragma unroll
+    for (int j = 0; j < CI / 16; ++j) accw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int t) {
+    const int cur = t & 1;
+    const uint16_t* Db = Ds + cur * BMT * CO;
+    f32x4 accd = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int mrow = rh * 16 + li;
+    const int wr = cq * 16 + li;
+#pragma unroll 8
+    for (int ks = 0; ks < CO / 32; ++ks) {
+      const int lch = ks * 4 + g;
+      const bf16x8 bfr = *(const bf16x8*)(Db + mrow * CO + tr_swz<CO>(mrow, lch * 8));
+      const bf16x8 af = *(const bf16x8*)(Ws + wr * CO + ((lch ^ (wr & 7)) * 8));
+      accd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, accd, 0, 0, 0);
+    }
+    wgrad_mma<CO, CI, 8, 1, 1>(Db, Xs + cur * BMT * CI, accw);
+    const int m = mbeg + t * BMT + mrow;
+    const uint16_t* xr = Xr + cur * BMT * CI + mrow * CI;
+    const int ci = cq * 16 + 4 * g;
+    const u32x2 yv = *(const u32x2*)(xr + ci);
+    const float4 tsc = *(const float4*)(Tb + ci), tsh = *(const float4*)(Tb + CI + ci);
+    const float4 tmu = *(const float4*)(Tb + 2 * CI + ci);
+    const float4 tin = *(const float4*)(Tb + 3 * CI + ci);
+    const float y[4] = {lo_bf(yv.x), hi_bf(yv.x), lo_bf(yv.y), hi_bf(yv.y)};
+    const float sc4[4] = {tsc.x, tsc.y, tsc.z, tsc.w}, sh4[4] = {tsh.x, tsh.y, tsh.z, tsh.w};
+    const float mu4[4] = {tmu.x, tmu.y, tmu.z, tmu.w}, in4[4] = {tin.x, tin.y, tin.z, tin.w};
+    float gv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a = bf2f(f2bf(accd[r]));
+      gv[r] = y[r] * sc4[r] + sh4[r] > 0.f ? a : 0.f;
+      s1[r] += gv[r];
+      s2[r] += gv[r] * ((y[r] - mu4[r]) * in4[r]);
+    }
+    const u32x2 w = {pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
+    __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CIT + c0 + ci));
+  };
+
+  __syncthreads();  // tables in LDS
+  if (T > 0) {
+    gload(0, rG[0], rA[0], rX[0]);
+    lstore(0, rG[0], rA[0], rX[0]);
+  }
+  if (T > 1) gload(1, rG[1], rA[1], rX[1]);
+  __syncthreads();
+  // raw barriers (LDS counter only), as in conv1x1_bwd_dual: a vmcnt(0) would drain the loads
+  // of tile t + 2 issued at the top of the iteration
+  for (int t = 0; t < T; t += 2) {
+    if (t + 2 < T) gload(t + 2, rG[0], rA[0], rX[0]);
+    compute(t);
+    if (t + 1 < T) lstore(1, rG[1], rA[1], rX[1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 1 >= T) break;
+    if (t + 3 < T) gload(t + 3, rG[1], rA[1], rX[1]);
+    compute(t + 1);
+    if (t + 2 < T) lstore(0, rG[0], rA[0], rX[0]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  __syncthreads();
+  float* wp = p.wpart + (size_t)blk * CO * CIT;
+#pragma unroll
+  for (int fm = 0; fm < CO / 8 / 16; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < CI / 16; ++fn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        wp[(size_t)(wid * (CO / 8) + fm * 16 + g * 4 + i) * CIT + c0 + fn * 16 + li] =
+            accw[fm][fn][i];
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[r] += __shfl_xor(s1[r], off, 64);
+      s2[r] += __shfl_xor(s2[r], off, 64);
+    }
+  if (li == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ci = cq * 16 + 4 * g + r;
+      red[(rh * CI + ci) * 2 + 0] = s1[r];
+      red[(rh * CI + ci) * 2 + 1] = s2[r];
+    }
+  }
+  __syncthreads();
+  if (tid < CI) {
+    const float a = red[tid * 2 + 0] + red[(CI + tid) * 2 + 0];
+    const float b = red[tid * 2 + 1] + red[(CI + tid) * 2 + 1];
+    p.stats[((size_t)blk * 2 + 0) * CIT + c0 + tid] = a;
+    p.stats[((size_t)blk * 2 + 1) * CIT + c0 + tid] = b;
   }
 }
 
@@ -3405,10 +3610,15 @@ size_t conv1x1_bwd_dual_lds() {
          (size_t)4 * 64 * 2 * 4 + (size_t)4 * 64 * 4;
 }
 
+size_t conv1x1_bwd_dual_w_lds(int CO) {
+  return (size_t)2 * 32 * CO * 2 + (size_t)2 * 2 * 32 * 64 * 2 + (size_t)64 * CO * 2 +
+         (size_t)2 * 64 * 2 * 4 + (size_t)4 * 64 * 4 + (size_t)3 * CO * 4;
+}
+
 void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, const uint16_t* X,
                       const float* xss, const float* xmi, const uint16_t* Wt, uint16_t* gm,
                       float* stats, float* wpart, int M, int CO, int CI, int S, int bps,
-                      hipStream_t s) {
+                      hipStream_t s, const uint16_t* Xraw) {
   Dual1x1Args a{};
   a.G = G; a.A3 = A3; a.coef = coef; a.X = X; a.xss = xss; a.xmi = xmi; a.Wt = Wt; a.gm = gm;
   a.stats = stats; a.wpart = wpart;
@@ -3416,8 +3626,22 @@ void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, 
   a.tiles_per_block = a.seg_rows / 64 / bps;
   a.g_bytes = (uint32_t)((size_t)M * CO * 2);
   a.x_bytes = (uint32_t)((size_t)M * CI * 2);
+  a.Xraw = Xraw;
+  a.x_pre = Xraw != nullptr;
   const size_t lds = conv1x1_bwd_dual_lds();
-  if (CO == 256 && CI == 64) {
+  if (CO == 512 && CI == 128) {
+    a.tiles_per_block = a.seg_rows / 32 / bps;  // 32-row m-tiles
+    const dim3 grid(S * bps * 2), blk(512);
+    const size_t wl = conv1x1_bwd_dual_w_lds(512);
+    if (A3 != nullptr && Xraw != nullptr)
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, true, true>), grid, blk, wl, s, a);
+    else if (A3 != nullptr)
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, true, false>), grid, blk, wl, s, a);
+    else if (Xraw != nullptr)
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, false, true>), grid, blk, wl, s, a);
+    else
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, false, false>), grid, blk, wl, s, a);
+  } else if (CO == 256 && CI == 64 && Xraw == nullptr) {
     hipLaunchKernelGGL((conv1x1_bwd_dual<256, 64>), dim3(S * bps), dim3(256), lds, s, a);
   } else {
     fprintf(stderr, "conv1x1_bwd_dual: unsupported Co=%d Ci=%d\n", CO, CI);

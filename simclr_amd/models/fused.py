@@ -196,6 +196,10 @@ class FusedStages:
         # pass (conv.hip conv1x1_bwd_dual): dgrad + BN2 mask / partials + weight gradient, so the
         # 0.5-1 GB output gradient is read once instead of once per pass
         self.fused_bwd1x1 = True
+        # ... and the wide form at Ci = 128 / Co = 512 (ResNet-50 layer2 conv3; conv.hip
+        # conv1x1_bwd_dual_w: the Ci slices of a row range share each dY tile through L2), which
+        # also takes the forward's materialised BN2+ReLU input (_mat_expand) as its X operand
+        self.fused_bwd1x1_wide = True
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -485,10 +489,10 @@ class FusedStages:
             run()
 
     @staticmethod
-    def _bwd1x1_bps(rows_seg: int) -> int:
+    def _bwd1x1_bps(rows_seg: int, cap: int = _BWD1X1_BPS) -> int:
         """Persistent blocks per view segment of conv1x1_bwd_dual (64-row tiles, equal shares)."""
         tiles = rows_seg // 64
-        b = min(_BWD1X1_BPS, tiles)
+        b = min(cap, tiles)
         while b > 1 and tiles % b:
             b -= 1
         return b
@@ -496,19 +500,32 @@ class FusedStages:
     def _bwd1x1_ok(self, cs: _ConvSpec, dyn: torch.Tensor, xin: torch.Tensor, pro_ss, a_prev,
                    S: int) -> bool:
         M = dyn.numel() // dyn.shape[-1]
-        return (getattr(self, "fused_bwd1x1", False) and cs.k == 1 and cs.stride == 1
-                and cs.conv.out_channels == 256 and cs.conv.in_channels == 64
-                and xin is a_prev and pro_ss is not None
-                and M % S == 0 and (M // S) % 64 == 0 and M * 256 * 2 < (1 << 31))
+        if not (getattr(self, "fused_bwd1x1", False) and cs.k == 1 and cs.stride == 1
+                and M % S == 0 and (M // S) % 64 == 0):
+            return False
+        co, ci = cs.conv.out_channels, cs.conv.in_channels
+        if (co, ci) == (256, 64):
+            return xin is a_prev and pro_ss is not None and M * 256 * 2 < (1 << 31)
+        if (co, ci) == (512, 128) and getattr(self, "fused_bwd1x1_wide", False):
+            # X: a2 with the BN2 prologue, or the forward's materialised relu(bn2(a2))
+            return ((xin is a_prev and pro_ss is not None)
+                    or (pro_ss is None and xin.shape == a_prev.shape)) and M * 512 * 2 < (1 << 31)
+        return False
 
-    def _bwd1x1_fused(self, ops, dyn, bnb, cs: _ConvSpec, a_prev, bs_prev: _BNState, S: int):
+    def _bwd1x1_fused(self, ops, dyn, bnb, cs: _ConvSpec, a_prev, bs_prev: _BNState, S: int,
+                      xin: Optional[torch.Tensor] = None):
         """conv3 dgrad (mode-3 epilogue of BN2) + weight gradient in one launch; the weight
         gradient's split reduction runs on the side stream.  Returns (gm, partials, blocks per
-        segment) like ``_dgrad`` with ``bn_epi=("mask", ...)``."""
+        segment) like ``_dgrad`` with ``bn_epi=("mask", ...)``.  ``xin``: the conv's forward
+        input when it was materialised (relu(bn2(a2)); wide form only)."""
         Nb, H, W, Ci = a_prev.shape
         Co = cs.conv.out_channels
         M = Nb * H * W
-        bps = self._bwd1x1_bps(M // S)
+        wide = (Co, Ci) == (512, 128)
+        # the wide kernel launches 2 blocks (Ci slices) per row block: 64 row blocks per view
+        # segment fill the chip's 256 CUs once at S = 2
+        bps = self._bwd1x1_bps(M // S, 64 if wide else _BWD1X1_BPS)
+        xraw = xin if (wide and xin is not None and xin is not a_prev) else None
         w = shadow_ohwi(cs.conv.weight, Ci)
         wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
         dev = dyn.device
@@ -516,8 +533,12 @@ class FusedStages:
         stats = torch.empty((S * bps * 2 * Ci,), device=dev, dtype=torch.float32)
         wpart = torch.empty((S * bps * Co * Ci,), device=dev, dtype=torch.float32)
         a3, coef = (bnb[0], bnb[1]) if bnb is not None else (None, None)
-        ops.conv1x1_bwd_dual(dyn, a3, coef, a_prev, bs_prev.ss.view(-1), bs_prev.mi.view(-1), wt,
-                             gm, stats, wpart, S, bps)
+        if xraw is not None:  # X = the materialised relu(bn2(a2)); a2 for the epilogue
+            ops.conv1x1_bwd_dual(dyn, a3, coef, xraw, bs_prev.ss.view(-1), bs_prev.mi.view(-1),
+                                 wt, gm, stats, wpart, S, bps, a_prev)
+        else:
+            ops.conv1x1_bwd_dual(dyn, a3, coef, a_prev, bs_prev.ss.view(-1),
+                                 bs_prev.mi.view(-1), wt, gm, stats, wpart, S, bps)
 
         def run():
             if _SKIP_WGRAD:
@@ -1102,7 +1123,7 @@ class FusedStages:
                 self._wgrad(ops, dy_m, xin, cs, pro_ss, S)
             elif self._bwd1x1_ok(cs, dyn, xin, pro_ss, a_prev, S):
                 _ext.TAG = f"{b.name} conv{i + 1} dgrad+wgrad"
-                gm, part, nb = self._bwd1x1_fused(ops, dyn, bnb, cs, a_prev, bs_prev, S)
+                gm, part, nb = self._bwd1x1_fused(ops, dyn, bnb, cs, a_prev, bs_prev, S, xin)
                 h = self._bn_bwd_start(ops, b.convs[i - 1].bn, part, nb, bs_prev, S, st)
             else:
                 gm, part, nb = self._dgrad(ops, dyn, cs, a_prev.shape, S,

@@ -138,14 +138,16 @@ class Recorder:
             orig["_wgrad"](self_, ops, dyn, xn, cs, pro_ss, S, bnb, main)
             rec._maybe_mutate(self_, cs, main)
 
-        def bwd1x1(self_, ops, dyn, bnb, cs, a_prev, bs_prev, S):
-            res = orig["_bwd1x1_fused"](self_, ops, dyn, bnb, cs, a_prev, bs_prev, S)
+        def bwd1x1(self_, ops, dyn, bnb, cs, a_prev, bs_prev, S, xin=None):
+            res = orig["_bwd1x1_fused"](self_, ops, dyn, bnb, cs, a_prev, bs_prev, S, xin)
             gm = res[0]
             rec.dgrads.append(dict(cs=cs, dyn=dyn, in_shape=tuple(a_prev.shape),
                                    accumulate=False, bn_epi=("mask", a_prev, bs_prev), bnb=bnb,
                                    compact=False, sub_resid=False, dx_prev=None, resid=None,
                                    out=gm, bnb_out=None))
-            rec.wgrads.append(dict(cs=cs, dyn=dyn, xn=a_prev, pro_ss=bs_prev.ss, bnb=bnb))
+            pre = xin is not None and xin is not a_prev  # the forward's materialised input
+            rec.wgrads.append(dict(cs=cs, dyn=dyn, xn=xin if pre else a_prev,
+                                   pro_ss=None if pre else bs_prev.ss, bnb=bnb))
             rec._maybe_mutate(self_, cs, False)
             return res
 

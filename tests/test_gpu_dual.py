@@ -66,3 +66,57 @@ def test_conv1x1_bwd_dual_matches_fp32(Nb, H, lazy, bps):
     assert _rel(st[:, 0], ref_s1) < 2e-3, _rel(st[:, 0], ref_s1)
     assert _rel(st[:, 1], ref_s2) < 2e-3, _rel(st[:, 1], ref_s2)
     assert _rel(dW, dW_ref) < 2e-3, _rel(dW, dW_ref)
+
+
+@pytest.mark.parametrize("Nb,H,lazy,pre,bps", [(64, 16, True, True, 64), (64, 16, True, False, 64),
+                                               (32, 16, False, True, 32), (16, 8, False, False, 8),
+                                               (1024, 16, True, True, 64)])
+def test_conv1x1_bwd_dual_wide_matches_fp32(Nb, H, lazy, pre, bps):
+    """The wide form (Co = 512, Ci = 128: ResNet-50 layer2 conv3; two 64-channel Ci slices per
+    row block, 32-row tiles, 8 waves) with and without the lazy BN3 prologue, with X either
+    BN2-applied in the kernel or the forward's materialised relu(bn2(a2)) (``Xraw`` = a2 for the
+    epilogue), against fp32 torch: dX with the BN2 mask, the BN2-backward partials, dW.
+    (1024, 16): the production layer2 shape (512 images x 2 views)."""
+    from simclr_amd.ops import _ext
+    ops = _ext.ops()
+    torch.manual_seed(Nb + H + int(lazy) + 2 * int(pre))
+    S, Co, Ci = 2, 512, 128
+    M = Nb * H * H
+    seg = M // S
+    G = _bf(torch.randn(M, Co, device=DEV))
+    A3 = _bf(torch.randn(M, Co, device=DEV)) if lazy else None
+    coef = torch.randn(3, S, Co, device=DEV) * 0.5 if lazy else None
+    X = _bf(torch.randn(M, Ci, device=DEV))              # a2 (pre-BN)
+    ss = torch.stack([0.5 + torch.rand(S, Ci, device=DEV), torch.randn(S, Ci, device=DEV) * 0.3])
+    mi = torch.stack([torch.randn(S, Ci, device=DEV) * 0.1, 0.5 + torch.rand(S, Ci, device=DEV)])
+    W = _bf(torch.randn(Co, Ci, device=DEV) * 0.04)
+    Wt = W.t().contiguous()
+    sg = torch.arange(M, device=DEV) // seg
+    Xf = X.float()
+    Xp = _bf(torch.relu(Xf * ss[0][sg] + ss[1][sg]))    # what the forward materialises
+    gm = torch.full((M, Ci), float("nan"), device=DEV, dtype=torch.bfloat16)
+    stats = torch.full((S * bps * 2 * Ci,), float("nan"), device=DEV)
+    wpart = torch.full((S * bps * Co * Ci,), float("nan"), device=DEV)
+    ops.conv1x1_bwd_dual(G, A3, coef.reshape(-1) if lazy else None, Xp if pre else X,
+                         ss.reshape(-1), mi.reshape(-1), Wt, gm, stats, wpart, S, bps,
+                         X if pre else None)
+    dW = torch.empty(Co, Ci, device=DEV)
+    ops.wgrad_reduce_slabs(wpart, S * bps, dW)
+    torch.cuda.synchronize()
+    if lazy:
+        dY = _bf(coef[0][sg] * G.float() + coef[1][sg] * A3.float() + coef[2][sg]).float()
+    else:
+        dY = G.float()
+    dX = _bf(dY @ W.float()).float()
+    mask = (Xf * ss[0][sg] + ss[1][sg]) > 0
+    g = torch.where(mask, dX, torch.zeros_like(dX))
+    xh = (Xf - mi[0][sg]) * mi[1][sg]
+    st = stats.view(S, bps, 2, Ci).sum(1)
+    ref_s1 = torch.stack([g[sg == s].sum(0) for s in range(S)])
+    ref_s2 = torch.stack([(g * xh)[sg == s].sum(0) for s in range(S)])
+    dW_ref = dY.t() @ Xp.float()
+    assert _rel(gm, g) < 1e-2, _rel(gm, g)
+    assert int(((gm.float() != 0) & ~mask).sum()) == 0
+    assert _rel(st[:, 0], ref_s1) < 2e-3, _rel(st[:, 0], ref_s1)
+    assert _rel(st[:, 1], ref_s2) < 2e-3, _rel(st[:, 1], ref_s2)
+    assert _rel(dW, dW_ref) < 2e-3, _rel(dW, dW_ref)
