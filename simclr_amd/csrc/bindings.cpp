@@ -350,8 +350,9 @@ void wgrad(const Tensor& dY, const Tensor& X, const Tensor& partial, const Tenso
 // fused 1x1 backward of a bottleneck conv3 (conv.hip conv1x1_bwd_dual): returns nothing; writes
 // gm [M][Ci], stats [S*bps][2][Ci] (BN2-backward partials), wpart [S*bps][Co][Ci] (dW slabs)
 void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
-                         const c10::optional<Tensor>& coef, const Tensor& X, const Tensor& xss,
-                         const Tensor& xmi, const Tensor& Wt, const Tensor& gm,
+                         const c10::optional<Tensor>& coef, const Tensor& X,
+                         const c10::optional<Tensor>& xss, const c10::optional<Tensor>& xmi,
+                         const Tensor& Wt, const Tensor& gm,
                          const Tensor& stats, const Tensor& wpart, int64_t S, int64_t bps,
                          const c10::optional<Tensor>& Xraw) {
   const int64_t CI = gm.size(-1);
@@ -366,8 +367,17 @@ void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
               "conv1x1_bwd_dual: operand sizes");
   TORCH_CHECK(S >= 1 && S <= 2 && bps >= 1 && M % S == 0 && (M / S) % (64 * bps) == 0,
               "conv1x1_bwd_dual: every block's rows must lie in one segment (64-row tiles)");
-  TORCH_CHECK(xss.numel() >= 2 * S * CI && xmi.numel() >= 2 * S * CI, "conv1x1_bwd_dual: BN2 tables");
-  TORCH_CHECK(stats.numel() >= S * bps * 2 * CI, "conv1x1_bwd_dual: stats size");
+  const float* xs = optf32(xss, "xss");
+  const float* xm = optf32(xmi, "xmi");
+  // no BN2 tables: the plain form (a downsample conv; no mask, no partials) — (256, 64) only
+  TORCH_CHECK((xs == nullptr) == (xm == nullptr), "conv1x1_bwd_dual: xss and xmi together");
+  TORCH_CHECK(xs != nullptr || (CO == 256 && CI == 64 && xr == nullptr),
+              "conv1x1_bwd_dual: the plain form is (Co, Ci) = (256, 64) only");
+  if (xs != nullptr) {
+    TORCH_CHECK(xss->numel() >= 2 * S * CI && xmi->numel() >= 2 * S * CI,
+                "conv1x1_bwd_dual: BN2 tables");
+    TORCH_CHECK(stats.numel() >= S * bps * 2 * CI, "conv1x1_bwd_dual: stats size");
+  }
   TORCH_CHECK(wpart.numel() >= S * bps * CO * CI, "conv1x1_bwd_dual: wpart size");
   TORCH_CHECK(M * CO * 2 < (int64_t(1) << 31), "conv1x1_bwd_dual: 32-bit buffer offsets");
   const uint16_t* a3 = optbf(A3, "A3");
@@ -376,7 +386,7 @@ void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
     TORCH_CHECK(A3->numel() == G.numel() && cf != nullptr && coef->numel() >= 3 * S * CO,
                 "conv1x1_bwd_dual: lazy BN-backward needs A3 [M][Co] and coef [3][S][Co]");
   }
-  conv1x1_bwd_dual(bf(G, "G"), a3, cf, bf(X, "X"), f32(xss, "xss"), f32(xmi, "xmi"),
+  conv1x1_bwd_dual(bf(G, "G"), a3, cf, bf(X, "X"), xs, xm,
                    bf(Wt, "Wt"), bfw(gm, "gm"), f32w(stats, "stats"), f32w(wpart, "wpart"),
                    (int)M, (int)CO, (int)CI, (int)S, (int)bps, cur_stream(), xr);
 }
@@ -1019,7 +1029,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("wgrad_variant_ok(int v, int[] geom, bool pro, bool dy_pro) -> bool", &wgrad_vok);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad_tiles(int[] geom, int variant=-1) -> int", &wgrad_ntiles);
-  m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor xss, Tensor xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps, Tensor? Xraw=None) -> ()", &conv1x1_bwd_dual_op);
+  m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor? xss, Tensor? xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps, Tensor? Xraw=None) -> ()", &conv1x1_bwd_dual_op);
   m.def("wgrad_reduce_slabs(Tensor(a!) partial, int splits, Tensor(b!) out, float beta=0.0) -> ()", &wgrad_reduce_slabs_op);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);

@@ -2861,7 +2861,10 @@ struct Dual1x1Args {
   int x_pre;
 };
 
-template <int CO, int CI>
+// PLAIN (a stride-1 downsample conv of the same shape, layer1.0): no BatchNorm between its input
+// and the conv — X is taken as stored, the dgrad output is written unmasked and no partials are
+// produced; with the lazy prologue its dY is the downsample BN's backward (A·g + B·ad + D).
+template <int CO, int CI, bool PLAIN = false>
 __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
   static_assert(CO == 256 && CI == 64, "tile mapping written for Co = 256, Ci = 64");
   constexpr int BMT = 64;  // rows per m-tile
@@ -2906,11 +2909,11 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
     cA[e] = lazy ? p.coef[seg * CO + co] : 1.f;
     cB[e] = lazy ? p.coef[(p.S + seg) * CO + co] : 0.f;
     cD[e] = lazy ? p.coef[(2 * p.S + seg) * CO + co] : 0.f;
-    xsc[e] = p.xss[seg * CI + ci];
-    xsh[e] = p.xss[(p.S + seg) * CI + ci];
+    xsc[e] = PLAIN ? 1.f : p.xss[seg * CI + ci];
+    xsh[e] = PLAIN ? 0.f : p.xss[(p.S + seg) * CI + ci];
   }
   // epilogue tables (BN2 scale, shift, mean, invstd of this segment) in LDS: [4][CI]
-  for (int i = tid; i < 4 * CI; i += 256) {
+  for (int i = tid; i < (PLAIN ? 0 : 4 * CI); i += 256) {
     const int k = i / CI, c = i % CI;
     Tb[i] = (k < 2 ? p.xss : p.xmi)[((k & 1) * p.S + seg) * CI + c];
   }
@@ -2943,8 +2946,8 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
     for (int j = 0; j < 2; ++j) {
       const int r = xrow + 32 * j;
       *(u32x4*)(Xs + buf * BMT * CI + r * CI + tr_swz<CI>(r, xch * 8)) =
-          affine_relu8(X2[j], xsc, xsh, true, true);
-      *(u32x4*)(Xr + buf * BMT * CI + r * CI + xch * 8) = X2[j];
+          PLAIN ? X2[j] : affine_relu8(X2[j], xsc, xsh, true, true);
+      if (!PLAIN) *(u32x4*)(Xr + buf * BMT * CI + r * CI + xch * 8) = X2[j];
     }
   };
 
@@ -2982,8 +2985,17 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
     }
     // wgrad: accw[fm][fn] += dY^T · X  (wave owns co = wid*64 .. +64)
     wgrad_mma<CO, CI, 4, 1>(Db, Xs + cur * BMT * CI, accw);
-    // mode-3 epilogue: g = [bn2(a2) > 0] · round(dX), Σg, Σg·x̂
     const int m = mbeg + t * BMT + mrow;
+    if constexpr (PLAIN) {
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        const int ci = fn * 16 + 4 * g;
+        const u32x2 w = {pack2bf(accd[fn][0], accd[fn][1]), pack2bf(accd[fn][2], accd[fn][3])};
+        __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CI + ci));
+      }
+      return;
+    }
+    // mode-3 epilogue: g = [bn2(a2) > 0] · round(dX), Σg, Σg·x̂
     const uint16_t* xr = Xr + cur * BMT * CI + mrow * CI;
 #pragma unroll
     for (int fn = 0; fn < 4; ++fn) {
@@ -3041,6 +3053,7 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         wp[(size_t)(wid * 64 + fm * 16 + g * 4 + i) * CI + fn * 16 + li] = accw[fm][fn][i];
+  if (PLAIN) return;
   // statistics: lanes sharing channels (same g) sum over li, then the 4 waves through LDS
 #pragma unroll
   for (int off = 1; off < 16; off <<= 1)
@@ -3641,6 +3654,8 @@ void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, 
       hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, false, true>), grid, blk, wl, s, a);
     else
       hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, false, false>), grid, blk, wl, s, a);
+  } else if (CO == 256 && CI == 64 && xss == nullptr) {
+    hipLaunchKernelGGL((conv1x1_bwd_dual<256, 64, true>), dim3(S * bps), dim3(256), lds, s, a);
   } else if (CO == 256 && CI == 64 && Xraw == nullptr) {
     hipLaunchKernelGGL((conv1x1_bwd_dual<256, 64>), dim3(S * bps), dim3(256), lds, s, a);
   } else {

@@ -200,6 +200,13 @@ class FusedStages:
         # conv1x1_bwd_dual_w: the Ci slices of a row range share each dY tile through L2), which
         # also takes the forward's materialised BN2+ReLU input (_mat_expand) as its X operand
         self.fused_bwd1x1_wide = True
+        # a stride-1 1x1 downsample of that shape (layer1.0, Co 256 / Ci 64) whose BatchNorm
+        # backward is lazy: its dgrad and weight gradient from one pass over g and its pre-BN
+        # activation (the plain form of conv1x1_bwd_dual) instead of a BN-apply pass writing
+        # its input gradient, a dgrad and a weight gradient each reading it; on the main stream
+        # ("main") or the downsample branch stream ("branch")
+        self.fused_ds_dual = True
+        self.ds_dual_stream = "main"
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
         self._wt_sig = None
@@ -212,12 +219,19 @@ class FusedStages:
         # separate reduce pass over the 1024 x 32 x 32 x 64 stem activation, no materialised
         # input gradient (stem_forward / backward)
         # A/B of the fusion switches above without code edits (tools/envab.sh):
-        # SIMCLR_FUSED_ATTRS="attr=value,..." (ints / true / false), applied at construction
+        # SIMCLR_FUSED_ATTRS="attr=value,..." (ints / true / false / strings), applied at
+        # construction
         for kv in filter(None, os.environ.get("SIMCLR_FUSED_ATTRS", "").split(",")):
             k, v = kv.split("=", 1)
             if not hasattr(self, k):
                 raise ValueError(f"SIMCLR_FUSED_ATTRS: FusedStages has no switch {k!r}")
-            setattr(self, k, v.lower() == "true" if v.lower() in ("true", "false") else int(v))
+            if v.lower() in ("true", "false"):
+                setattr(self, k, v.lower() == "true")
+            else:
+                try:
+                    setattr(self, k, int(v))
+                except ValueError:
+                    setattr(self, k, v)
         self.stem_fused = type(self).STEM_FUSED
         self.stem = None
         self._stem_block = None
@@ -556,6 +570,56 @@ class FusedStages:
             with torch.cuda.stream(side):
                 run()
         return gm, stats, bps
+
+    def _ds_dual_ok(self, b: _BlockSpec, tp: _BlockTape, S: int) -> bool:
+        """A stride-1 1x1 downsample of the narrow dual shape whose input needs no transform
+        (the block input) and whose dgrad covers every input position."""
+        cs = b.down
+        if not (getattr(self, "fused_ds_dual", False) and getattr(self, "fused_bwd1x1", False)
+                and tp.x.is_cuda and cs.k == 1 and cs.stride == 1 and cs.pad == 0
+                and b.convs[0].stride == 1):
+            return False
+        Nb, H, W, Ci = tp.x.shape
+        M = Nb * H * W
+        return ((cs.conv.out_channels, cs.conv.in_channels) == (256, 64) and Ci == 64
+                and M % S == 0 and (M // S) % 64 == 0 and M * 256 * 2 < (1 << 31))
+
+    def _ds_dual(self, ops, b: _BlockSpec, tp: _BlockTape, lazy_d, S: int) -> torch.Tensor:
+        """The downsample's input gradient (the residual of conv1's dgrad) and weight gradient
+        from one pass over g3 and the pre-BN activation ad, the downsample BN's backward applied
+        in registers (conv1x1_bwd_dual, plain form).  The weight gradient's split reduction runs
+        on the weight-gradient stream."""
+        cs = b.down
+        g3, coefd = lazy_d
+        Nb, H, W, Ci = tp.x.shape
+        Co = cs.conv.out_channels
+        M = Nb * H * W
+        bps = self._bwd1x1_bps(M // S)
+        w = shadow_ohwi(cs.conv.weight, Ci)
+        wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
+        dev = g3.device
+        _ext.TAG = f"{b.name} ds dgrad+wgrad"
+        resid = _empty_nhwc(Nb, H, W, Ci, dev)
+        wpart = torch.empty((S * bps * Co * Ci,), device=dev, dtype=torch.float32)
+        nostats = torch.empty((1,), device=dev, dtype=torch.float32)
+        ops.conv1x1_bwd_dual(g3, tp.ad, coefd, tp.x, None, None, wt, resid, nostats, wpart, S,
+                             bps)
+
+        def run():
+            if _SKIP_WGRAD:
+                _deliver_grad(cs.conv.weight, lambda out: None)
+                return
+            _deliver_grad(cs.conv.weight, lambda out: ops.wgrad_reduce_slabs(wpart, S * bps, out))
+
+        side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
+        if side is None:
+            run()
+        else:
+            self._side_keep.append(wpart)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                run()
+        return resid
 
     def _bnb_ok(self, cs: _ConvSpec, a: torch.Tensor, S: int) -> bool:
         """The BN-backward operand prologue applies to a 1x1 stride-1 conv whose per-segment
@@ -1065,9 +1129,9 @@ class FusedStages:
                 else:
                     ops.bn_bwd_apply(g3, None, aL, coefL, S, False, da, None)
         dad = None
+        ds_dual = None  # (g3, coefd): the downsample's backward as one fused pass (_ds_dual)
         if b.down is not None:
             _ext.TAG = f"{b.name} bnds bwd"
-            dad = torch.empty_like(tp.ad)
             if pre is not None and hd is not None:
                 # both BNs of the block output from one pass over g3 (their partials came
                 # from the following block's dgrad epilogue) — or only the downsample BN's,
@@ -1075,10 +1139,16 @@ class FusedStages:
                 coefd = self._bn_bwd_finish(ops, hd, S)
                 if self._lazy_bn3_ds_ok(b, tp, aL, S):
                     lazy = (aL, coefL)
-                    ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
+                    if self._ds_dual_ok(b, tp, S):
+                        ds_dual = (g3, coefd)  # dad never materialised
+                    else:
+                        dad = torch.empty_like(tp.ad)
+                        ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
                 else:
+                    dad = torch.empty_like(tp.ad)
                     ops.bn_bwd_apply2(g3, aL, coefL, da, tp.ad, coefd, dad, S)
             else:
+                dad = torch.empty_like(tp.ad)
                 nblk_d = ops.bn_blocks(R, C, S)
                 partial_d = torch.empty((S * nblk_d * 2 * C,), device=dev, dtype=torch.float32)
                 ops.bn_bwd_reduce(g3, None, tp.ad, tp.bnd.mi, S, False, partial_d)
@@ -1092,8 +1162,15 @@ class FusedStages:
         # position; a BasicBlock's conv1 carries the stride itself)
         compact = (b.down is not None and self.compact_ds and b.down.stride == 2 and b.down.k == 1
                    and b.down.pad == 0 and b.convs[0].stride == 1)
-        br = self._branch_stream(dad) if dad is not None else None
-        if br is not None:
+        br = self._branch_stream(tp.ad) if b.down is not None else None
+        if ds_dual is not None:
+            if br is not None and getattr(self, "ds_dual_stream", "main") == "branch":
+                br.wait_stream(torch.cuda.current_stream(tp.ad.device))
+                with torch.cuda.stream(br):
+                    resid_f = self._ds_dual(ops, b, tp, ds_dual, S)
+            else:
+                resid = self._ds_dual(ops, b, tp, ds_dual, S)
+        elif br is not None:
             # the downsample dgrad only meets the conv chain at conv1's dgrad epilogue
             br.wait_stream(torch.cuda.current_stream(dad.device))
             with torch.cuda.stream(br):
@@ -1146,9 +1223,9 @@ class FusedStages:
         cs0 = b.convs[0]
         if b.down is not None:
             if resid_f is not None:
-                torch.cuda.current_stream(dad.device).wait_stream(br)  # join
+                torch.cuda.current_stream(tp.ad.device).wait_stream(br)  # join
                 resid = resid_f
-            else:
+            elif ds_dual is None:
                 _ext.TAG = f"{b.name} ds dgrad"
                 resid, _, _ = self._dgrad(ops, dad, b.down, tp.x.shape, S, compact=compact)
         else:
@@ -1175,7 +1252,7 @@ class FusedStages:
                 h = (self._bn_bwd_start(ops, pb.convs[-1].bn, part, nb, ptp.bns[-1], S, st), None)
         _ext.TAG = f"{b.name} conv1 wgrad"
         self._wgrad(ops, da, tp.x, cs0, None, S, bnb=lazy0)
-        if b.down is not None:
+        if b.down is not None and ds_dual is None:
             _ext.TAG = f"{b.name} ds wgrad"
             self._wgrad(ops, dad, tp.x, b.down, None, S)
         _ext.TAG = ""

@@ -97,7 +97,7 @@ class Recorder:
         rec = self
         orig = {n: getattr(FusedStages, n) for n in
                 ("forward", "stem_forward", "_bn_fwd", "_dgrad", "_wgrad", "_bwd1x1_fused",
-                 "_bn_bwd_finish", "_block_backward")}
+                 "_bn_bwd_finish", "_block_backward", "_ds_dual")}
 
         def forward(self_, xn):
             out, tapes = orig["forward"](self_, xn)
@@ -151,6 +151,17 @@ class Recorder:
             rec._maybe_mutate(self_, cs, False)
             return res
 
+        def ds_dual(self_, ops, b, tp, lazy_d, S):
+            resid = orig["_ds_dual"](self_, ops, b, tp, lazy_d, S)
+            g3, coefd = lazy_d
+            rec.dgrads.append(dict(cs=b.down, dyn=g3, in_shape=tuple(tp.x.shape),
+                                   accumulate=False, bn_epi=None, bnb=(tp.ad, coefd),
+                                   compact=False, sub_resid=False, dx_prev=None, resid=None,
+                                   out=resid.clone(), bnb_out=None))
+            rec.wgrads.append(dict(cs=b.down, dyn=g3, xn=tp.x, pro_ss=None, bnb=(tp.ad, coefd)))
+            rec._maybe_mutate(self_, b.down, False)
+            return resid
+
         def bn_bwd_finish(self_, ops, h, S):
             coef = orig["_bn_bwd_finish"](self_, ops, h, S)
             rec.coefs.append(dict(bn=h[1], bs=h[4], coef=coef))
@@ -166,7 +177,8 @@ class Recorder:
 
         for n, f in (("forward", forward), ("stem_forward", stem_forward), ("_bn_fwd", bn_fwd),
                      ("_dgrad", dgrad), ("_wgrad", wgrad), ("_bwd1x1_fused", bwd1x1),
-                     ("_bn_bwd_finish", bn_bwd_finish), ("_block_backward", block_backward)):
+                     ("_bn_bwd_finish", bn_bwd_finish), ("_block_backward", block_backward),
+                     ("_ds_dual", ds_dual)):
             monkeypatch.setattr(FusedStages, n, f)
 
     def _name_convs(self, ex):

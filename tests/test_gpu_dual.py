@@ -120,3 +120,37 @@ def test_conv1x1_bwd_dual_wide_matches_fp32(Nb, H, lazy, pre, bps):
     assert _rel(st[:, 0], ref_s1) < 2e-3, _rel(st[:, 0], ref_s1)
     assert _rel(st[:, 1], ref_s2) < 2e-3, _rel(st[:, 1], ref_s2)
     assert _rel(dW, dW_ref) < 2e-3, _rel(dW, dW_ref)
+
+
+@pytest.mark.parametrize("Nb,H,lazy,bps", [(64, 8, True, 32), (32, 32, True, 128),
+                                           (32, 16, False, 64)])
+def test_conv1x1_bwd_dual_plain_matches_fp32(Nb, H, lazy, bps):
+    """The plain form (a stride-1 1x1 downsample, layer1.0: no BatchNorm between its input and
+    the conv, so no X transform, no mask, no partials): dX = dY · W unmasked and dW = dYᵀ · X,
+    with dY the downsample BN's backward A·g + B·ad + D formed in registers, vs fp32 torch."""
+    from simclr_amd.ops import _ext
+    ops = _ext.ops()
+    torch.manual_seed(Nb * H + int(lazy))
+    S, Co, Ci = 2, 256, 64
+    M = Nb * H * H
+    seg = M // S
+    G = _bf(torch.randn(M, Co, device=DEV))
+    A3 = _bf(torch.randn(M, Co, device=DEV)) if lazy else None
+    coef = torch.randn(3, S, Co, device=DEV) * 0.5 if lazy else None
+    X = _bf(torch.relu(torch.randn(M, Ci, device=DEV)))  # a block input (post-ReLU)
+    W = _bf(torch.randn(Co, Ci, device=DEV) * 0.06)
+    Wt = W.t().contiguous()
+    gm = torch.full((M, Ci), float("nan"), device=DEV, dtype=torch.bfloat16)
+    wpart = torch.full((S * bps * Co * Ci,), float("nan"), device=DEV)
+    ops.conv1x1_bwd_dual(G, A3, coef.reshape(-1) if lazy else None, X, None, None, Wt, gm,
+                         torch.empty(1, device=DEV), wpart, S, bps)
+    dW = torch.empty(Co, Ci, device=DEV)
+    ops.wgrad_reduce_slabs(wpart, S * bps, dW)
+    torch.cuda.synchronize()
+    sg = torch.arange(M, device=DEV) // seg
+    if lazy:
+        dY = _bf(coef[0][sg] * G.float() + coef[1][sg] * A3.float() + coef[2][sg]).float()
+    else:
+        dY = G.float()
+    assert _rel(gm, dY @ W.float()) < 1e-2, _rel(gm, dY @ W.float())
+    assert _rel(dW, dY.t() @ X.float()) < 2e-3, _rel(dW, dY.t() @ X.float())
