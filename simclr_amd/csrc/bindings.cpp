@@ -391,6 +391,33 @@ void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
                    (int)M, (int)CO, (int)CI, (int)S, (int)bps, cur_stream(), xr);
 }
 
+// 1x1 stride-2 downsample backward (layer2.0): X [N][H][W][Ci] block input, gm [N][OH][OW][Ci]
+void conv1x1_bwd_dual_s2_op(const Tensor& G, const c10::optional<Tensor>& A3,
+                            const c10::optional<Tensor>& coef, const Tensor& X, const Tensor& Wt,
+                            const Tensor& gm, const Tensor& wpart, int64_t S, int64_t bps) {
+  TORCH_CHECK(X.dim() == 4 && gm.dim() == 4, "conv1x1_bwd_dual_s2: NHWC 4-D X and gm");
+  const int64_t N = X.size(0), H = X.size(1), W = X.size(2), CI = X.size(3);
+  const int64_t OH = gm.size(1), OW = gm.size(2);
+  TORCH_CHECK(gm.size(0) == N && gm.size(3) == CI && OH == (H + 1) / 2 && OW == (W + 1) / 2,
+              "conv1x1_bwd_dual_s2: gm is the stride-2 output map");
+  const int64_t Mo = N * OH * OW;
+  const int64_t CO = G.numel() / Mo;
+  TORCH_CHECK(CO == 512 && CI == 256 && G.numel() == Mo * CO && Wt.numel() == CI * CO,
+              "conv1x1_bwd_dual_s2: (Co, Ci) = (512, 256) only");
+  TORCH_CHECK(S >= 1 && S <= 2 && N % S == 0 && bps >= 1 && (Mo / S) % (64 * bps) == 0,
+              "conv1x1_bwd_dual_s2: every block's rows must lie in one segment");
+  TORCH_CHECK(wpart.numel() >= S * bps * CO * CI, "conv1x1_bwd_dual_s2: wpart size");
+  TORCH_CHECK(Mo * CO * 2 < (int64_t(1) << 31) && X.numel() * 2 < (int64_t(1) << 31),
+              "conv1x1_bwd_dual_s2: 32-bit buffer offsets");
+  const uint16_t* a3 = optbf(A3, "A3");
+  const float* cf = optf32(coef, "coef");
+  TORCH_CHECK(a3 == nullptr && cf == nullptr,
+              "conv1x1_bwd_dual_s2: dY must be materialised (no lazy BN-backward form)");
+  conv1x1_bwd_dual_s2(bf(G, "G"), a3, cf, bf(X, "X"), bf(Wt, "Wt"), bfw(gm, "gm"),
+                      f32w(wpart, "wpart"), (int)Mo, (int)CO, (int)CI, (int)S, (int)bps, (int)H,
+                      (int)W, (int)OH, (int)OW, cur_stream());
+}
+
 void wgrad_reduce_slabs_op(const Tensor& partial, int64_t splits, const Tensor& out, double beta) {
   const int64_t n = out.numel();
   TORCH_CHECK(n % 4 == 0 && partial.numel() >= splits * n && splits >= 1,
@@ -1029,6 +1056,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("wgrad_variant_ok(int v, int[] geom, bool pro, bool dy_pro) -> bool", &wgrad_vok);
   m.def("wgrad_splits(int[] geom, int variant=-1) -> int", &wgrad_nsplit);
   m.def("wgrad_tiles(int[] geom, int variant=-1) -> int", &wgrad_ntiles);
+  m.def("conv1x1_bwd_dual_s2(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor Wt, "
+        "Tensor(a!) gm, Tensor(b!) wpart, int S, int bps) -> ()", &conv1x1_bwd_dual_s2_op);
   m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor? xss, Tensor? xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps, Tensor? Xraw=None) -> ()", &conv1x1_bwd_dual_op);
   m.def("wgrad_reduce_slabs(Tensor(a!) partial, int splits, Tensor(b!) out, float beta=0.0) -> ()", &wgrad_reduce_slabs_op);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);

@@ -2859,6 +2859,9 @@ struct Dual1x1Args {
   // the epilogue's mask / x̂
   const uint16_t* Xraw;
   int x_pre;
+  // plain stride-2 downsample form (conv1x1_bwd_dual_s2): X is the [N][xH][xW][Ci] block input,
+  // output pixel (n, oh, ow) of the xOH x xOW map reads input pixel (n, 2 oh, 2 ow)
+  int xH, xW, xOH, xOW;
 };
 
 // PLAIN (a stride-1 downsample conv of the same shape, layer1.0): no BatchNorm between its input
@@ -3100,13 +3103,17 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
 // X is either a2 with BN2 + ReLU applied while staging (XPRE = false) or the forward's
 // materialised relu(bn2(a2)) (XPRE, a2 read beside it for the epilogue).  The per-channel
 // tables live in LDS (registers are the constraint here).
-template <int CO, int CIT, bool LAZY, bool XPRE>
+// PLAIN: a 1x1 stride-2 downsample conv (layer2.0: Co 512, Ci 256) — no BatchNorm between its
+// input and the conv, so X is read as stored (at the even positions of the block input, XS2),
+// the dgrad output (the compact residual of conv1's dgrad) is written unmasked, no partials.
+template <int CO, int CIT, bool LAZY, bool XPRE, bool PLAIN = false, bool XS2 = false>
 __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
   constexpr int CI = 64;   // channels of Ci per block
   constexpr int NH = CIT / CI;
   constexpr int BMT = 32;  // rows per m-tile
   constexpr int NT = 512;
   static_assert(CO == 512 && CIT % CI == 0, "wide dual tile mapping (64 output channels per wave)");
+  static_assert(!XS2 || PLAIN, "the strided X form is the plain downsample form");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* Ds = (uint16_t*)smem;          // [2][32][CO]  tr_swz<CO> image of dY
   uint16_t* Xs = Ds + 2 * BMT * CO;        // [2][32][CI]  tr_swz<CI> image of relu(bn2(a2)) (slice)
@@ -3141,7 +3148,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
     *(u32x4*)(Ws + row * CO + ((ch ^ (row & 7)) * 8)) =
         *(const u32x4*)(p.Wt + ((size_t)(c0 + row) * CO + ch * 8));
   }
-  for (int i = tid; i < 4 * CI; i += NT) {
+  for (int i = tid; i < (PLAIN ? 0 : 4 * CI); i += NT) {
     const int k = i / CI, c = i % CI;
     Tb[i] = (k < 2 ? p.xss : p.xmi)[((k & 1) * p.S + seg) * CIT + c0 + c];
   }
@@ -3156,9 +3163,17 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
   static_assert(256 / XCH == BMT, "one X chunk per thread (of the first 256) per tile");
   const int gch = tid % GCH, grow = tid / GCH;
   const int xt = tid & 255, xch = xt % XCH, xrow = xt / XCH;
-  const bool xload = XPRE || wid < 4;
+  const bool xload = (XPRE && !PLAIN) || wid < 4;
 
   u32x4 rG[2][GJ], rA[2][GJ], rX[2];
+  uint32_t xs_n = 0, xs_oh = 0, xs_ow = 0;  // XS2: the lane's output pixel of the next gload
+  if (XS2) {
+    const uint32_t m = (uint32_t)(mbeg + xrow), ohw = (uint32_t)(p.xOH * p.xOW);
+    xs_n = m / ohw;
+    const uint32_t rem = m - xs_n * ohw;
+    xs_oh = rem / (uint32_t)p.xOW;
+    xs_ow = rem - xs_oh * (uint32_t)p.xOW;
+  }
   auto gload = [&](int t, u32x4 (&G8)[GJ], u32x4 (&A8)[GJ], u32x4& X1) {
     const int m0 = mbeg + t * BMT;
 #pragma unroll
@@ -3167,9 +3182,19 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
       G8[j] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
       if (LAZY) A8[j] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
     }
-    if (xload)
+    if (xload) {
+      uint32_t xr_ = (uint32_t)(m0 + xrow);  // (the binding bounds every offset by 2^31)
+      if constexpr (XS2) {
+        // output pixel -> the input pixel at (2 oh, 2 ow); gload runs in tile order, so the
+        // lane's (n, oh, ow) advances by one tile (BMT output pixels) per call
+        xr_ = (xs_n * (uint32_t)p.xH + 2u * xs_oh) * (uint32_t)p.xW + 2u * xs_ow;
+        xs_ow += BMT;
+        while (xs_ow >= (uint32_t)p.xOW) { xs_ow -= (uint32_t)p.xOW; ++xs_oh; }
+        while (xs_oh >= (uint32_t)p.xOH) { xs_oh -= (uint32_t)p.xOH; ++xs_n; }
+      }
       X1 = __builtin_amdgcn_raw_buffer_load_b128(
-          rx, (uint32_t)(((size_t)(m0 + xrow) * CIT + c0 + xch * 8) * 2), 0, 0);
+          rx, (xr_ * (uint32_t)CIT + (uint32_t)(c0 + xch * 8)) * 2u, 0, 0);
+    }
   };
   auto lstore = [&](int buf, const u32x4 (&G8)[GJ], const u32x4 (&A8)[GJ], const u32x4& X1) {
 #pragma unroll
@@ -3182,9 +3207,9 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
     }
     if (wid < 4) {
       *(u32x4*)(Xs + buf * BMT * CI + xrow * CI + tr_swz<CI>(xrow, xch * 8)) =
-          XPRE ? X1 : affine_relu8(X1, Tb + xch * 8, Tb + CI + xch * 8, true, true);
-      if (!XPRE) *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
-    } else if (XPRE) {
+          (XPRE || PLAIN) ? X1 : affine_relu8(X1, Tb + xch * 8, Tb + CI + xch * 8, true, true);
+      if (!XPRE && !PLAIN) *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
+    } else if (XPRE && !PLAIN) {
       *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
     }
   };
@@ -3202,7 +3227,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
     f32x4 accd = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int mrow = rh * 16 + li;
     const int wr = cq * 16 + li;
-#pragma unroll 8
+#pragma unroll 4
     for (int ks = 0; ks < CO / 32; ++ks) {
       const int lch = ks * 4 + g;
       const bf16x8 bfr = *(const bf16x8*)(Db + mrow * CO + tr_swz<CO>(mrow, lch * 8));
@@ -3211,6 +3236,11 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
     }
     wgrad_mma<CO, CI, 8, 1, 1>(Db, Xs + cur * BMT * CI, accw);
     const int m = mbeg + t * BMT + mrow;
+    if constexpr (PLAIN) {
+      const int ci = cq * 16 + 4 * g;
+      const u32x2 w = {pack2bf(accd[0], accd[1]), pack2bf(accd[2], accd[3])};
+      __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CIT + c0 + ci));
+    } else {
     const uint16_t* xr = Xr + cur * BMT * CI + mrow * CI;
     const int ci = cq * 16 + 4 * g;
     const u32x2 yv = *(const u32x2*)(xr + ci);
@@ -3230,6 +3260,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
     }
     const u32x2 w = {pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
     __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CIT + c0 + ci));
+    }
   };
 
   __syncthreads();  // tables in LDS
@@ -3243,13 +3274,17 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
   // of tile t + 2 issued at the top of the iteration
   for (int t = 0; t < T; t += 2) {
     if (t + 2 < T) gload(t + 2, rG[0], rA[0], rX[0]);
+    if constexpr (PLAIN) __builtin_amdgcn_sched_barrier(0);  // (keeps the loads' live ranges)
     compute(t);
+    if constexpr (PLAIN) __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < T) lstore(1, rG[1], rA[1], rX[1]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + 1 >= T) break;
     if (t + 3 < T) gload(t + 3, rG[1], rA[1], rX[1]);
+    if constexpr (PLAIN) __builtin_amdgcn_sched_barrier(0);
     compute(t + 1);
+    if constexpr (PLAIN) __builtin_amdgcn_sched_barrier(0);
     if (t + 2 < T) lstore(0, rG[0], rA[0], rX[0]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -3264,6 +3299,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
       for (int i = 0; i < 4; ++i)
         wp[(size_t)(wid * (CO / 8) + fm * 16 + g * 4 + i) * CIT + c0 + fn * 16 + li] =
             accw[fm][fn][i];
+  if (PLAIN) return;
 #pragma unroll
   for (int off = 1; off < 16; off <<= 1)
 #pragma unroll
@@ -3662,6 +3698,32 @@ void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, 
     fprintf(stderr, "conv1x1_bwd_dual: unsupported Co=%d Ci=%d\n", CO, CI);
     abort();  // the bindings reject this
   }
+  HIP_CHECK_LAUNCH();
+}
+
+// layer2.0's 1x1 stride-2 downsample backward (Co 512, Ci 256): compact input gradient and
+// weight-gradient slabs from one pass over g and ad (lazy BN backward when A3 is given)
+void conv1x1_bwd_dual_s2(const uint16_t* G, const uint16_t* A3, const float* coef,
+                         const uint16_t* X, const uint16_t* Wt, uint16_t* gm, float* wpart,
+                         int Mo, int CO, int CI, int S, int bps, int H, int W, int OH, int OW,
+                         hipStream_t s) {
+  Dual1x1Args a{};
+  a.G = G; a.A3 = A3; a.coef = coef; a.X = X; a.Wt = Wt; a.gm = gm; a.wpart = wpart;
+  a.M = Mo; a.S = S; a.seg_rows = Mo / S; a.bps = bps;
+  a.tiles_per_block = a.seg_rows / 32 / bps;
+  a.g_bytes = (uint32_t)((size_t)Mo * CO * 2);
+  a.x_bytes = (uint32_t)((size_t)(Mo / (OH * OW)) * H * W * CI * 2);
+  a.xH = H; a.xW = W; a.xOH = OH; a.xOW = OW;
+  if (CO != 512 || CI != 256) {
+    fprintf(stderr, "conv1x1_bwd_dual_s2: unsupported Co=%d Ci=%d\n", CO, CI);
+    abort();  // the bindings reject this
+  }
+  const dim3 grid(S * bps * (CI / 64)), blk(512);
+  const size_t wl = conv1x1_bwd_dual_w_lds(512);
+  // (the lazy-prologue instantiation of this form spilled 58 VGPRs at 8 waves: the caller
+  // materialises dY, the binding rejects A3)
+  hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 256, false, false, true, true>), grid, blk, wl, s,
+                     a);
   HIP_CHECK_LAUNCH();
 }
 

@@ -85,6 +85,10 @@ void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, 
                       const float* xss, const float* xmi, const uint16_t* Wt, uint16_t* gm,
                       float* stats, float* wpart, int M, int CO, int CI, int S, int bps,
                       hipStream_t s, const uint16_t* Xraw = nullptr);
+void conv1x1_bwd_dual_s2(const uint16_t* G, const uint16_t* A3, const float* coef,
+                         const uint16_t* X, const uint16_t* Wt, uint16_t* gm, float* wpart,
+                         int Mo, int CO, int CI, int S, int bps, int H, int W, int OH, int OW,
+                         hipStream_t s);
 void wgrad_reduce_slabs(float* partial, int splits, float* out, size_t n, float beta,
                         hipStream_t s);
 // output tiles of a weight-gradient launch (ticket words of the in-kernel split reduction)

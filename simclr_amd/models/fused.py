@@ -206,6 +206,9 @@ class FusedStages:
         # its input gradient, a dgrad and a weight gradient each reading it; on the main stream
         # ("main") or the downsample branch stream ("branch")
         self.fused_ds_dual = True
+        # ... and layer2.0's stride-2 downsample (Co 512 / Ci 256, dY materialised): measured
+        # neutral to +0.06 ms (r6 log), so off by default
+        self.fused_ds_dual_s2 = False
         self.ds_dual_stream = "main"
         self._side_keep: List[torch.Tensor] = []
         # dgrad weight transforms of the whole backbone: one batched launch per backward
@@ -572,17 +575,24 @@ class FusedStages:
         return gm, stats, bps
 
     def _ds_dual_ok(self, b: _BlockSpec, tp: _BlockTape, S: int) -> bool:
-        """A stride-1 1x1 downsample of the narrow dual shape whose input needs no transform
-        (the block input) and whose dgrad covers every input position."""
+        """A 1x1 downsample whose input needs no transform (the block input): stride 1 at the
+        narrow dual shape (Co 256 / Ci 64, lazy BN backward), or stride 2 at Co 512 / Ci 256
+        (layer2.0; dY materialised: ``_ds_dual_s2``)."""
         cs = b.down
         if not (getattr(self, "fused_ds_dual", False) and getattr(self, "fused_bwd1x1", False)
-                and tp.x.is_cuda and cs.k == 1 and cs.stride == 1 and cs.pad == 0
-                and b.convs[0].stride == 1):
+                and tp.x.is_cuda and cs.k == 1 and cs.pad == 0 and b.convs[0].stride == 1):
             return False
         Nb, H, W, Ci = tp.x.shape
-        M = Nb * H * W
-        return ((cs.conv.out_channels, cs.conv.in_channels) == (256, 64) and Ci == 64
-                and M % S == 0 and (M // S) % 64 == 0 and M * 256 * 2 < (1 << 31))
+        shape = (cs.conv.out_channels, cs.conv.in_channels)
+        if cs.stride == 1:
+            M = Nb * H * W
+            return (shape == (256, 64) and Ci == 64 and M % S == 0 and (M // S) % 64 == 0
+                    and M * 256 * 2 < (1 << 31))
+        if cs.stride == 2 and getattr(self, "fused_ds_dual_s2", False):
+            Mo = Nb * ((H + 1) // 2) * ((W + 1) // 2)
+            return (shape == (512, 256) and Ci == 256 and Nb % S == 0 and (Mo // S) % 64 == 0
+                    and Mo * 512 * 2 < (1 << 31) and tp.x.numel() * 2 < (1 << 31))
+        return False
 
     def _ds_dual(self, ops, b: _BlockSpec, tp: _BlockTape, lazy_d, S: int) -> torch.Tensor:
         """The downsample's input gradient (the residual of conv1's dgrad) and weight gradient
@@ -593,17 +603,30 @@ class FusedStages:
         g3, coefd = lazy_d
         Nb, H, W, Ci = tp.x.shape
         Co = cs.conv.out_channels
-        M = Nb * H * W
-        bps = self._bwd1x1_bps(M // S)
-        w = shadow_ohwi(cs.conv.weight, Ci)
-        wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
         dev = g3.device
         _ext.TAG = f"{b.name} ds dgrad+wgrad"
-        resid = _empty_nhwc(Nb, H, W, Ci, dev)
-        wpart = torch.empty((S * bps * Co * Ci,), device=dev, dtype=torch.float32)
-        nostats = torch.empty((1,), device=dev, dtype=torch.float32)
-        ops.conv1x1_bwd_dual(g3, tp.ad, coefd, tp.x, None, None, wt, resid, nostats, wpart, S,
-                             bps)
+        if cs.stride == 2:
+            # layer2.0: dY materialised (the lazy form of the wide kernel spills), then ONE pass
+            # for the compact input gradient and the weight gradient (strided X)
+            OH, OW = (H + 1) // 2, (W + 1) // 2
+            dad = torch.empty_like(tp.ad)
+            ops.bn_bwd_apply(g3, None, tp.ad, coefd, S, False, dad, None)
+            bps = self._bwd1x1_bps(Nb * OH * OW // S, 32)
+            w = shadow_ohwi(cs.conv.weight, Ci)
+            wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, 2, 0, 2])
+            resid = _empty_nhwc(Nb, OH, OW, Ci, dev)
+            wpart = torch.empty((S * bps * Co * Ci,), device=dev, dtype=torch.float32)
+            ops.conv1x1_bwd_dual_s2(dad, None, None, tp.x, wt, resid, wpart, S, bps)
+        else:
+            M = Nb * H * W
+            bps = self._bwd1x1_bps(M // S)
+            w = shadow_ohwi(cs.conv.weight, Ci)
+            wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
+            resid = _empty_nhwc(Nb, H, W, Ci, dev)
+            wpart = torch.empty((S * bps * Co * Ci,), device=dev, dtype=torch.float32)
+            nostats = torch.empty((1,), device=dev, dtype=torch.float32)
+            ops.conv1x1_bwd_dual(g3, tp.ad, coefd, tp.x, None, None, wt, resid, nostats, wpart,
+                                 S, bps)
 
         def run():
             if _SKIP_WGRAD:

@@ -156,8 +156,8 @@ class Recorder:
             g3, coefd = lazy_d
             rec.dgrads.append(dict(cs=b.down, dyn=g3, in_shape=tuple(tp.x.shape),
                                    accumulate=False, bn_epi=None, bnb=(tp.ad, coefd),
-                                   compact=False, sub_resid=False, dx_prev=None, resid=None,
-                                   out=resid.clone(), bnb_out=None))
+                                   compact=b.down.stride == 2, sub_resid=False, dx_prev=None,
+                                   resid=None, out=resid.clone(), bnb_out=None))
             rec.wgrads.append(dict(cs=b.down, dyn=g3, xn=tp.x, pro_ss=None, bnb=(tp.ad, coefd)))
             rec._maybe_mutate(self_, b.down, False)
             return resid

@@ -154,3 +154,34 @@ def test_conv1x1_bwd_dual_plain_matches_fp32(Nb, H, lazy, bps):
         dY = G.float()
     assert _rel(gm, dY @ W.float()) < 1e-2, _rel(gm, dY @ W.float())
     assert _rel(dW, dY.t() @ X.float()) < 2e-3, _rel(dW, dY.t() @ X.float())
+
+
+@pytest.mark.parametrize("Nb,H,bps", [(16, 8, 2), (64, 32, 32), (1024, 32, 32)])
+def test_conv1x1_bwd_dual_s2_matches_fp32(Nb, H, bps):
+    """The strided plain wide form (layer2.0's 1x1 stride-2 downsample, Co 512 / Ci 256): the
+    compact input gradient (the even input positions only) and the weight gradient from one
+    pass over dY, X read at the even positions of the block input, vs fp32 torch conv2d
+    gradients.  (1024, 32): the production shape."""
+    import torch.nn.functional as F
+    from simclr_amd.ops import _ext
+    ops = _ext.ops()
+    torch.manual_seed(Nb + H)
+    S, Co, Ci = 2, 512, 256
+    OH = (H + 1) // 2
+    Mo = Nb * OH * OH
+    X = _bf(torch.relu(torch.randn(Nb, H, H, Ci, device=DEV)))
+    dY = _bf(torch.randn(Nb, OH, OH, Co, device=DEV))
+    W = _bf(torch.randn(Co, Ci, device=DEV) * 0.04)
+    Wt = W.t().contiguous()
+    gm = torch.full((Nb, OH, OH, Ci), float("nan"), device=DEV, dtype=torch.bfloat16)
+    wpart = torch.full((S * bps * Co * Ci,), float("nan"), device=DEV)
+    ops.conv1x1_bwd_dual_s2(dY, None, None, X, Wt, gm, wpart, S, bps)
+    dW = torch.empty(Co, Ci, device=DEV)
+    ops.wgrad_reduce_slabs(wpart, S * bps, dW)
+    torch.cuda.synchronize()
+    xr = X.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = W.float().view(Co, Ci, 1, 1).requires_grad_(True)
+    F.conv2d(xr, wr, None, 2, 0).backward(dY.float().permute(0, 3, 1, 2))
+    ref_dx = xr.grad.permute(0, 2, 3, 1)[:, ::2, ::2, :]
+    assert _rel(gm, ref_dx) < 1e-2, _rel(gm, ref_dx)
+    assert _rel(dW, wr.grad.view(Co, Ci)) < 2e-3, _rel(dW, wr.grad.view(Co, Ci))
