@@ -354,7 +354,7 @@ void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
                          const c10::optional<Tensor>& xss, const c10::optional<Tensor>& xmi,
                          const Tensor& Wt, const Tensor& gm,
                          const Tensor& stats, const Tensor& wpart, int64_t S, int64_t bps,
-                         const c10::optional<Tensor>& Xraw) {
+                         const c10::optional<Tensor>& Xraw, bool dual8) {
   const int64_t CI = gm.size(-1);
   const int64_t M = gm.numel() / CI;
   const int64_t CO = G.numel() / M;
@@ -388,7 +388,7 @@ void conv1x1_bwd_dual_op(const Tensor& G, const c10::optional<Tensor>& A3,
   }
   conv1x1_bwd_dual(bf(G, "G"), a3, cf, bf(X, "X"), xs, xm,
                    bf(Wt, "Wt"), bfw(gm, "gm"), f32w(stats, "stats"), f32w(wpart, "wpart"),
-                   (int)M, (int)CO, (int)CI, (int)S, (int)bps, cur_stream(), xr);
+                   (int)M, (int)CO, (int)CI, (int)S, (int)bps, cur_stream(), xr, dual8);
 }
 
 // 1x1 stride-2 downsample backward (layer2.0): X [N][H][W][Ci] block input, gm [N][OH][OW][Ci]
@@ -1058,7 +1058,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("wgrad_tiles(int[] geom, int variant=-1) -> int", &wgrad_ntiles);
   m.def("conv1x1_bwd_dual_s2(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor Wt, "
         "Tensor(a!) gm, Tensor(b!) wpart, int S, int bps) -> ()", &conv1x1_bwd_dual_s2_op);
-  m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor? xss, Tensor? xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps, Tensor? Xraw=None) -> ()", &conv1x1_bwd_dual_op);
+  m.def("conv1x1_bwd_dual(Tensor G, Tensor? A3, Tensor? coef, Tensor X, Tensor? xss, Tensor? xmi, Tensor Wt, Tensor(a!) gm, Tensor(b!) stats, Tensor(c!) wpart, int S, int bps, Tensor? Xraw=None, bool dual8=False) -> ()", &conv1x1_bwd_dual_op);
   m.def("wgrad_reduce_slabs(Tensor(a!) partial, int splits, Tensor(b!) out, float beta=0.0) -> ()", &wgrad_reduce_slabs_op);
   m.def("wgrad(Tensor dY, Tensor X, Tensor(a!) partial, Tensor(b!) out, int[] geom, int splits, int creal, float beta, Tensor? pro_sc=None, Tensor? pro_sh=None, int pro_seg_rows=0, bool pro_relu=False, int pro_S=1, int variant=-1, Tensor? dY2=None, Tensor? dp_coef=None, int dp_seg_rows=0, int dp_S=1) -> ()", &wgrad);
   m.def("weight_transform(Tensor W, Tensor(a!) Wt, int[] p) -> ()", &weight_transform);

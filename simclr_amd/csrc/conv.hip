@@ -3106,27 +3106,36 @@ __global__ __launch_bounds__(256, 1) void conv1x1_bwd_dual(Dual1x1Args p) {
 // PLAIN: a 1x1 stride-2 downsample conv (layer2.0: Co 512, Ci 256) — no BatchNorm between its
 // input and the conv, so X is read as stored (at the even positions of the block input, XS2),
 // the dgrad output (the compact residual of conv1's dgrad) is written unmasked, no partials.
-template <int CO, int CIT, bool LAZY, bool XPRE, bool PLAIN = false, bool XS2 = false>
+// BMT = 64 with CO = 256 is the 8-wave form of the narrow kernel (Co 256 / Ci 64, one Ci slice):
+// two waves per SIMD overlap one wave's VALU / LDS work (the BN prologue, the epilogue) with the
+// other's MFMAs, where the 4-wave conv1x1_bwd_dual issues them in order.
+template <int CO, int CIT, bool LAZY, bool XPRE, bool PLAIN = false, bool XS2 = false,
+          int BMT = 32>
 __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
   constexpr int CI = 64;   // channels of Ci per block
   constexpr int NH = CIT / CI;
-  constexpr int BMT = 32;  // rows per m-tile
   constexpr int NT = 512;
-  static_assert(CO == 512 && CIT % CI == 0, "wide dual tile mapping (64 output channels per wave)");
+  constexpr int RG = BMT / 16;        // dgrad row groups of 16 rows
+  constexpr int CQ = 8 / RG;          // dgrad channel groups
+  constexpr int CW = CI / CQ;         // dgrad channels per wave
+  constexpr int NF = CW / 16;         // 16-channel fragments per wave
+  static_assert((CO == 512 && BMT == 32) || (CO == 256 && BMT == 64), "dual tile mappings");
+  static_assert(CIT % CI == 0 && NF >= 1, "dual tile mapping");
   static_assert(!XS2 || PLAIN, "the strided X form is the plain downsample form");
+  static_assert(!XPRE || BMT * (CI / 8) == 256, "XPRE: half the threads load the raw operand");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* Ds = (uint16_t*)smem;          // [2][32][CO]  tr_swz<CO> image of dY
   uint16_t* Xs = Ds + 2 * BMT * CO;        // [2][32][CI]  tr_swz<CI> image of relu(bn2(a2)) (slice)
   uint16_t* Xr = Xs + 2 * BMT * CI;        // [2][32][CI]  raw a2 (slice)
   uint16_t* Ws = Xr + 2 * BMT * CI;        // [CI][CO]     Wᵀ slice, chunk ^= row & 7
-  float* red = (float*)(Ws + CI * CO);     // [2 row halves][CI][2]
-  float* Tb = red + 2 * CI * 2;            // [4][CI]  BN2 scale, shift, mean, invstd (slice)
+  float* red = (float*)(Ws + CI * CO);     // [RG row groups][CI][2]
+  float* Tb = red + RG * CI * 2;           // [4][CI]  BN2 scale, shift, mean, invstd (slice)
   float* Cf = Tb + 4 * CI;                 // [3][CO]  BN3-backward A, B, D (LAZY)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar) selects
   const int g = lane >> 4, li = lane & 15;
-  const int rh = wid & 1, cq = wid >> 1;   // dgrad: row half, 16-channel quarter of the slice
+  const int rh = wid % RG, cq = wid / RG;  // dgrad: row group, channel group of the slice
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int half = lb % NH;
   const int blk = lb / NH;
@@ -3160,10 +3169,12 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
   constexpr int GCH = CO / 8, XCH = CI / 8;
   constexpr int GR = NT / GCH;         // dY rows per loader pass
   constexpr int GJ = BMT / GR;         // passes per tile
-  static_assert(256 / XCH == BMT, "one X chunk per thread (of the first 256) per tile");
+  constexpr int XT = BMT * XCH;        // X chunks per tile: 256 or 512 (one per thread)
+  static_assert(XT == 256 || XT == 512, "X chunk mapping");
   const int gch = tid % GCH, grow = tid / GCH;
-  const int xt = tid & 255, xch = xt % XCH, xrow = xt / XCH;
-  const bool xload = (XPRE && !PLAIN) || wid < 4;
+  const int xt = tid % XT, xch = xt % XCH, xrow = xt / XCH;
+  const bool xload = XT == 512 || (XPRE && !PLAIN) || wid < 4;
+  const bool xown = XT == 512 || wid < 4;  // this thread's chunk goes to Xs (else: raw, XPRE)
 
   u32x4 rG[2][GJ], rA[2][GJ], rX[2];
   uint32_t xs_n = 0, xs_oh = 0, xs_ow = 0;  // XS2: the lane's output pixel of the next gload
@@ -3205,7 +3216,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
                            true);
       *(u32x4*)(Ds + buf * BMT * CO + r * CO + tr_swz<CO>(r, gch * 8)) = v;
     }
-    if (wid < 4) {
+    if (xown) {
       *(u32x4*)(Xs + buf * BMT * CI + xrow * CI + tr_swz<CI>(xrow, xch * 8)) =
           (XPRE || PLAIN) ? X1 : affine_relu8(X1, Tb + xch * 8, Tb + CI + xch * 8, true, true);
       if (!XPRE && !PLAIN) *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
@@ -3219,30 +3230,40 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
   for (int i = 0; i < CO / 8 / 16; ++i)
 #pragma unroll
     for (int j = 0; j < CI / 16; ++j) accw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  float s1[NF][4], s2[NF][4];
+#pragma unroll
+  for (int fn = 0; fn < NF; ++fn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[fn][r] = 0.f; s2[fn][r] = 0.f; }
 
   auto compute = [&](int t) {
     const int cur = t & 1;
     const uint16_t* Db = Ds + cur * BMT * CO;
-    f32x4 accd = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x4 accd[NF];
+#pragma unroll
+    for (int fn = 0; fn < NF; ++fn) accd[fn] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int mrow = rh * 16 + li;
-    const int wr = cq * 16 + li;
 #pragma unroll 4
     for (int ks = 0; ks < CO / 32; ++ks) {
       const int lch = ks * 4 + g;
       const bf16x8 bfr = *(const bf16x8*)(Db + mrow * CO + tr_swz<CO>(mrow, lch * 8));
-      const bf16x8 af = *(const bf16x8*)(Ws + wr * CO + ((lch ^ (wr & 7)) * 8));
-      accd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, accd, 0, 0, 0);
+#pragma unroll
+      for (int fn = 0; fn < NF; ++fn) {
+        const int wr = cq * CW + fn * 16 + li;
+        const bf16x8 af = *(const bf16x8*)(Ws + wr * CO + ((lch ^ (wr & 7)) * 8));
+        accd[fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, accd[fn], 0, 0, 0);
+      }
     }
-    wgrad_mma<CO, CI, 8, 1, 1>(Db, Xs + cur * BMT * CI, accw);
+    wgrad_mma<CO, CI, 8, 1, BMT / 32>(Db, Xs + cur * BMT * CI, accw);
     const int m = mbeg + t * BMT + mrow;
+#pragma unroll
+    for (int fn = 0; fn < NF; ++fn) {
+    const int ci = cq * CW + fn * 16 + 4 * g;
     if constexpr (PLAIN) {
-      const int ci = cq * 16 + 4 * g;
-      const u32x2 w = {pack2bf(accd[0], accd[1]), pack2bf(accd[2], accd[3])};
+      const u32x2 w = {pack2bf(accd[fn][0], accd[fn][1]), pack2bf(accd[fn][2], accd[fn][3])};
       __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CIT + c0 + ci));
     } else {
     const uint16_t* xr = Xr + cur * BMT * CI + mrow * CI;
-    const int ci = cq * 16 + 4 * g;
     const u32x2 yv = *(const u32x2*)(xr + ci);
     const float4 tsc = *(const float4*)(Tb + ci), tsh = *(const float4*)(Tb + CI + ci);
     const float4 tmu = *(const float4*)(Tb + 2 * CI + ci);
@@ -3253,13 +3274,14 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
     float gv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float a = bf2f(f2bf(accd[r]));
+      const float a = bf2f(f2bf(accd[fn][r]));
       gv[r] = y[r] * sc4[r] + sh4[r] > 0.f ? a : 0.f;
-      s1[r] += gv[r];
-      s2[r] += gv[r] * ((y[r] - mu4[r]) * in4[r]);
+      s1[fn][r] += gv[r];
+      s2[fn][r] += gv[r] * ((y[r] - mu4[r]) * in4[r]);
     }
     const u32x2 w = {pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
     __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CIT + c0 + ci));
+    }
     }
   };
 
@@ -3303,22 +3325,30 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
 #pragma unroll
   for (int off = 1; off < 16; off <<= 1)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      s1[r] += __shfl_xor(s1[r], off, 64);
-      s2[r] += __shfl_xor(s2[r], off, 64);
-    }
+    for (int fn = 0; fn < NF; ++fn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[fn][r] += __shfl_xor(s1[fn][r], off, 64);
+        s2[fn][r] += __shfl_xor(s2[fn][r], off, 64);
+      }
   if (li == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ci = cq * 16 + 4 * g + r;
-      red[(rh * CI + ci) * 2 + 0] = s1[r];
-      red[(rh * CI + ci) * 2 + 1] = s2[r];
-    }
+    for (int fn = 0; fn < NF; ++fn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ci = cq * CW + fn * 16 + 4 * g + r;
+        red[(rh * CI + ci) * 2 + 0] = s1[fn][r];
+        red[(rh * CI + ci) * 2 + 1] = s2[fn][r];
+      }
   }
   __syncthreads();
   if (tid < CI) {
-    const float a = red[tid * 2 + 0] + red[(CI + tid) * 2 + 0];
-    const float b = red[tid * 2 + 1] + red[(CI + tid) * 2 + 1];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int q = 0; q < RG; ++q) {  // fixed order: deterministic
+      a += red[(q * CI + tid) * 2 + 0];
+      b += red[(q * CI + tid) * 2 + 1];
+    }
     p.stats[((size_t)blk * 2 + 0) * CIT + c0 + tid] = a;
     p.stats[((size_t)blk * 2 + 1) * CIT + c0 + tid] = b;
   }
@@ -3659,15 +3689,15 @@ size_t conv1x1_bwd_dual_lds() {
          (size_t)4 * 64 * 2 * 4 + (size_t)4 * 64 * 4;
 }
 
-size_t conv1x1_bwd_dual_w_lds(int CO) {
-  return (size_t)2 * 32 * CO * 2 + (size_t)2 * 2 * 32 * 64 * 2 + (size_t)64 * CO * 2 +
-         (size_t)2 * 64 * 2 * 4 + (size_t)4 * 64 * 4 + (size_t)3 * CO * 4;
+size_t conv1x1_bwd_dual_w_lds(int CO, int BMT = 32) {
+  return (size_t)2 * BMT * CO * 2 + (size_t)2 * 2 * BMT * 64 * 2 + (size_t)64 * CO * 2 +
+         (size_t)(BMT / 16) * 64 * 2 * 4 + (size_t)4 * 64 * 4 + (size_t)3 * CO * 4;
 }
 
 void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, const uint16_t* X,
                       const float* xss, const float* xmi, const uint16_t* Wt, uint16_t* gm,
                       float* stats, float* wpart, int M, int CO, int CI, int S, int bps,
-                      hipStream_t s, const uint16_t* Xraw) {
+                      hipStream_t s, const uint16_t* Xraw, bool dual8) {
   Dual1x1Args a{};
   a.G = G; a.A3 = A3; a.coef = coef; a.X = X; a.xss = xss; a.xmi = xmi; a.Wt = Wt; a.gm = gm;
   a.stats = stats; a.wpart = wpart;
@@ -3690,6 +3720,22 @@ void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, 
       hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, false, true>), grid, blk, wl, s, a);
     else
       hipLaunchKernelGGL((conv1x1_bwd_dual_w<512, 128, false, false>), grid, blk, wl, s, a);
+  } else if (CO == 256 && CI == 64 && Xraw == nullptr && dual8) {
+    // 8-wave form (64-row tiles)
+    const dim3 grid(S * bps), blk(512);
+    const size_t wl = conv1x1_bwd_dual_w_lds(256, 64);
+    if (xss == nullptr && A3 != nullptr)
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<256, 64, true, false, true, false, 64>), grid, blk,
+                         wl, s, a);
+    else if (xss == nullptr)
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<256, 64, false, false, true, false, 64>), grid, blk,
+                         wl, s, a);
+    else if (A3 != nullptr)
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<256, 64, true, false, false, false, 64>), grid, blk,
+                         wl, s, a);
+    else
+      hipLaunchKernelGGL((conv1x1_bwd_dual_w<256, 64, false, false, false, false, 64>), grid,
+                         blk, wl, s, a);
   } else if (CO == 256 && CI == 64 && xss == nullptr) {
     hipLaunchKernelGGL((conv1x1_bwd_dual<256, 64, true>), dim3(S * bps), dim3(256), lds, s, a);
   } else if (CO == 256 && CI == 64 && Xraw == nullptr) {

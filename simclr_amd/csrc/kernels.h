@@ -84,7 +84,7 @@ size_t conv1x1_bwd_dual_lds();
 void conv1x1_bwd_dual(const uint16_t* G, const uint16_t* A3, const float* coef, const uint16_t* X,
                       const float* xss, const float* xmi, const uint16_t* Wt, uint16_t* gm,
                       float* stats, float* wpart, int M, int CO, int CI, int S, int bps,
-                      hipStream_t s, const uint16_t* Xraw = nullptr);
+                      hipStream_t s, const uint16_t* Xraw = nullptr, bool dual8 = false);
 void conv1x1_bwd_dual_s2(const uint16_t* G, const uint16_t* A3, const float* coef,
                          const uint16_t* X, const uint16_t* Wt, uint16_t* gm, float* wpart,
                          int Mo, int CO, int CI, int S, int bps, int H, int W, int OH, int OW,

@@ -205,6 +205,10 @@ class FusedStages:
         # activation (the plain form of conv1x1_bwd_dual) instead of a BN-apply pass writing
         # its input gradient, a dgrad and a weight gradient each reading it; on the main stream
         # ("main") or the downsample branch stream ("branch")
+        # the narrow fused 1x1 backward (Co 256 / Ci 64) as the 8-wave kernel
+        # (conv1x1_bwd_dual_w, 64-row tiles) instead of the 4-wave one: -0.03..-0.08 ms/step,
+        # 3 of 3 rounds (r6 log)
+        self.dual8 = True
         self.fused_ds_dual = True
         # ... and layer2.0's stride-2 downsample (Co 512 / Ci 256, dY materialised): measured
         # neutral to +0.06 ms (r6 log), so off by default
@@ -555,7 +559,8 @@ class FusedStages:
                                  wt, gm, stats, wpart, S, bps, a_prev)
         else:
             ops.conv1x1_bwd_dual(dyn, a3, coef, a_prev, bs_prev.ss.view(-1),
-                                 bs_prev.mi.view(-1), wt, gm, stats, wpart, S, bps)
+                                 bs_prev.mi.view(-1), wt, gm, stats, wpart, S, bps,
+                                 dual8=bool(getattr(self, "dual8", False)))
 
         def run():
             if _SKIP_WGRAD:
@@ -626,7 +631,7 @@ class FusedStages:
             wpart = torch.empty((S * bps * Co * Ci,), device=dev, dtype=torch.float32)
             nostats = torch.empty((1,), device=dev, dtype=torch.float32)
             ops.conv1x1_bwd_dual(g3, tp.ad, coefd, tp.x, None, None, wt, resid, nostats, wpart,
-                                 S, bps)
+                                 S, bps, dual8=bool(getattr(self, "dual8", False)))
 
         def run():
             if _SKIP_WGRAD:

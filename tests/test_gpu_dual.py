@@ -18,9 +18,11 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
 
 
+@pytest.mark.parametrize("dual8", [False, True])
 @pytest.mark.parametrize("Nb,H,lazy,bps", [(64, 8, True, 32), (64, 8, False, 16),
                                            (32, 32, True, 128), (32, 32, False, 64)])
-def test_conv1x1_bwd_dual_matches_fp32(Nb, H, lazy, bps):
+def test_conv1x1_bwd_dual_matches_fp32(Nb, H, lazy, bps, dual8):
+    """(dual8: the same op as the 8-wave, 64-row-tile conv1x1_bwd_dual_w form.)"""
     from simclr_amd.ops import _ext
     ops = _ext.ops()
     torch.manual_seed(Nb + H + int(lazy))
@@ -39,7 +41,7 @@ def test_conv1x1_bwd_dual_matches_fp32(Nb, H, lazy, bps):
     stats = torch.empty(S * bps * 2 * Ci, device=DEV)
     wpart = torch.empty(S * bps * Co * Ci, device=DEV)
     ops.conv1x1_bwd_dual(G, A3, coef.reshape(-1) if lazy else None, X, ss.reshape(-1),
-                         mi.reshape(-1), Wt, gm, stats, wpart, S, bps)
+                         mi.reshape(-1), Wt, gm, stats, wpart, S, bps, dual8=dual8)
     dW = torch.empty(Co, Ci, device=DEV)
     ops.wgrad_reduce_slabs(wpart, S * bps, dW)
     torch.cuda.synchronize()
@@ -122,9 +124,10 @@ def test_conv1x1_bwd_dual_wide_matches_fp32(Nb, H, lazy, pre, bps):
     assert _rel(dW, dW_ref) < 2e-3, _rel(dW, dW_ref)
 
 
+@pytest.mark.parametrize("dual8", [False, True])
 @pytest.mark.parametrize("Nb,H,lazy,bps", [(64, 8, True, 32), (32, 32, True, 128),
                                            (32, 16, False, 64)])
-def test_conv1x1_bwd_dual_plain_matches_fp32(Nb, H, lazy, bps):
+def test_conv1x1_bwd_dual_plain_matches_fp32(Nb, H, lazy, bps, dual8):
     """The plain form (a stride-1 1x1 downsample, layer1.0: no BatchNorm between its input and
     the conv, so no X transform, no mask, no partials): dX = dY · W unmasked and dW = dYᵀ · X,
     with dY the downsample BN's backward A·g + B·ad + D formed in registers, vs fp32 torch."""
@@ -143,7 +146,7 @@ def test_conv1x1_bwd_dual_plain_matches_fp32(Nb, H, lazy, bps):
     gm = torch.full((M, Ci), float("nan"), device=DEV, dtype=torch.bfloat16)
     wpart = torch.full((S * bps * Co * Ci,), float("nan"), device=DEV)
     ops.conv1x1_bwd_dual(G, A3, coef.reshape(-1) if lazy else None, X, None, None, Wt, gm,
-                         torch.empty(1, device=DEV), wpart, S, bps)
+                         torch.empty(1, device=DEV), wpart, S, bps, dual8=dual8)
     dW = torch.empty(Co, Ci, device=DEV)
     ops.wgrad_reduce_slabs(wpart, S * bps, dW)
     torch.cuda.synchronize()
