@@ -209,6 +209,9 @@ class FusedStages:
         # (conv1x1_bwd_dual_w, 64-row tiles) instead of the 4-wave one: -0.03..-0.08 ms/step,
         # 3 of 3 rounds (r6 log)
         self.dual8 = True
+        # the fused 1x1 backward kernels' weight-gradient slab reduction on the main stream
+        # (serial, ~10 µs at the full chip) instead of the weight-gradient stream
+        self.dual_reduce_main = False
         self.fused_ds_dual = True
         # ... and layer2.0's stride-2 downsample (Co 512 / Ci 256, dY materialised): measured
         # neutral to +0.06 ms (r6 log), so off by default
@@ -570,6 +573,8 @@ class FusedStages:
                           lambda out: ops.wgrad_reduce_slabs(wpart, S * bps, out))
 
         side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
+        if getattr(self, "dual_reduce_main", False):
+            side = None
         if side is None:
             run()
         else:
@@ -640,6 +645,8 @@ class FusedStages:
             _deliver_grad(cs.conv.weight, lambda out: ops.wgrad_reduce_slabs(wpart, S * bps, out))
 
         side = getattr(self, "_side", None) if getattr(self, "wgrad_stream", False) else None
+        if getattr(self, "dual_reduce_main", False):
+            side = None
         if side is None:
             run()
         else:
