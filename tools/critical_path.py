@@ -1,7 +1,9 @@
 """Approximate critical path of one bench step from a rocprofv3 kernel trace.
 
 Walks back from the step's last kernel: the predecessor of a kernel is the kernel (any queue)
-whose end is the latest at or before that kernel's start (+1 µs of launch skew).  Prints the
+whose end is the latest at or before that kernel's start (+1 µs of launch skew); a same-queue
+kernel ending within 10 µs of that one is preferred (a side-queue kernel starved of CUs by it
+ends just after it).  Prints the
 chain's time per kernel family, the idle gaps along it, and the chain itself (last step).
 
 usage: python tools/critical_path.py run_kernel_trace.csv [--list]"""
@@ -30,6 +32,11 @@ def main():
         if not cands:
             break
         p = max(cands, key=lambda r: r[1])
+        # a side-queue kernel whose blocks only got CUs once a main-queue kernel drained ends a
+        # few µs after it: credit the same-queue kernel, the one that actually held the chip
+        same = [r for r in cands if r[3] == cur[3] and r[1] >= p[1] - 10000]
+        if same:
+            p = max(same, key=lambda r: r[1])
         chain.append(p)
         cur = p
     chain.reverse()
