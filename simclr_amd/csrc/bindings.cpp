@@ -282,6 +282,7 @@ bool igemm_gldsok(std::vector<int64_t> gv, bool pro, bool bn_bwd_pro) {
   return igemm_glds_ok(geom_from(gv), pro, bn_bwd_pro);
 }
 int64_t wgrad_nvariants() { return wgrad_num_variants(); }
+int64_t wgrad_xlin_op(int64_t mode) { return wgrad_xlin((int)mode); }
 bool wgrad_vglds(int64_t v) { return wgrad_variant_glds((int)v); }
 bool igemm_vok(int64_t v, std::vector<int64_t> gv, bool pro, bool bnb) {
   return igemm_variant_ok((int)v, geom_from(gv), pro, bnb);
@@ -1044,6 +1045,7 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("igemm_variant_glds(int v) -> bool", &igemm_vglds);
   m.def("igemm_glds_ok(int[] geom, bool pro, bool bn_bwd_pro) -> bool", &igemm_gldsok);
   m.def("wgrad_nvariants() -> int", &wgrad_nvariants);
+  m.def("wgrad_xlin(int mode=-1) -> int", &wgrad_xlin_op);
   m.def("wgrad_variant_glds(int v) -> bool", &wgrad_vglds);
   m.def("igemm_variant_patch(int v) -> bool", [](int64_t v) {
     return v >= 0 && v < igemm_num_variants() && igemm_variant_patch((int)v);

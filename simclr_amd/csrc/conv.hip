@@ -1201,6 +1201,7 @@ struct WgradArgs {
   const float* dp_coef;
   int dp_seg_rows, dp_S;
   size_t slab_stride;  // floats between split slabs (N*K; 0 only in the attribution experiment)
+  uint32_t x_step;     // wgrad_xp XLIN: X bytes per 64-row step (wgrad_x_linear)
 };
 
 // Weight-gradient MFMA shape: 16 = v_mfma_f32_16x16x32_bf16 (f32x4 accumulators), 32 =
@@ -1878,7 +1879,13 @@ __device__ __forceinline__ void wg_mma_ks(const WgKs<TCO, TKK, MF>& f,
 // live (the 256 x 256 tile fits without spilling).  The barrier also frees the step's buffer:
 // the DMA of step it + 2 is issued right after it (2 LDS stages, one step of DMA in flight, as
 // wgrad_glds).
-template <int BCO, int BKK, int WM, int WN, int MF>
+//
+// XLIN: every lane's X gather address advances by the same p.x_step per 64-row step with a fixed
+// validity (wgrad_x_linear: a 1x1 stride-1 unpadded conv, whose X rows are the output rows, or
+// an output image of OH*OW pixels dividing 64, whose rows keep their (oh, ow) and advance n).
+// The general form re-derives (n, oh, ow, ih, iw) and the bounds for every DMA piece of every
+// step: ~6 VALU per MFMA in the layer3 3x3 weight gradient (profiles/r6_wgrad_pmc.md).
+template <int BCO, int BKK, int WM, int WN, int MF, bool XLIN = false>
 __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_xp(WgradArgs p) {
   constexpr int NW = WM * WN;
   constexpr int CPD = BCO / 8, RPD = 64 / CPD, DI = 64 / (RPD * NW);
@@ -1943,6 +1950,19 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_xp(WgradArgs p) {
   const int dn = 64 / OHW, dr = 64 - dn * OHW;
   const int doh = dr / p.OW, dow = dr - doh * p.OW;
   const int cstride = p.C * 2;
+  uint32_t xl_off[XLIN ? XI : 1];
+  bool xl_ok[XLIN ? XI : 1];
+  if constexpr (XLIN) {
+#pragma unroll
+    for (int j = 0; j < XI; ++j) {
+      const int ih = xoh[j] * p.ish + x_ihb[j];
+      const int iw = xow[j] * p.isw + x_iwb[j];
+      xl_ok[j] = x_kok[j] && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      xl_off[j] = xl_ok[j] ? (uint32_t)((((size_t)xn[j] * p.IH + ih) * p.IW + iw) * cstride +
+                                        x_ci[j] * 2)
+                           : 0u;
+    }
+  }
 
   auto issue = [&](int it, int buf) {
     const int mb = mbeg + it * 64;
@@ -1952,6 +1972,16 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_xp(WgradArgs p) {
       dma16_opaque(rd, Ds + buf * 64 * BCO + (j * NW + wid) * RPD * BCO,
                    ok ? d_off[j] : p.dy_bytes);
       d_off[j] += dstep;
+    }
+    if constexpr (XLIN) {
+#pragma unroll
+      for (int j = 0; j < XI; ++j) {
+        const bool ok = mb + x_row[j] < mend && xl_ok[j];
+        dma16_opaque(rx, Xs + buf * 64 * BKK + (j * NW + wid) * RPX * BKK,
+                     ok ? xl_off[j] : p.x_bytes);
+        xl_off[j] += p.x_step;
+      }
+      return;
     }
 #pragma unroll
     for (int j = 0; j < XI; ++j) {
@@ -2750,6 +2780,33 @@ void launch_wgrad_pipe(const WgradArgs& a0, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+// X bytes per 64-row step when every X gather address of wgrad_xp is affine in the step with a
+// fixed validity, else 0 (see XLIN).  SIMCLR_WGRAD_XLIN: 0 = the general form everywhere (the
+// default), 1 = every admissible shape, 3 = the k x k (MFMA-bound) shapes only.  XLIN makes
+// every xp weight gradient 7-12 % faster alone, but the N = 1 step, where the weight gradients
+// run hidden on their side stream, was +0.05 ms slower over 10 interleaved rounds
+// (profiles/r6_wgrad_pmc.md), so it stays opt-in
+static int g_wgrad_xlin = -1;  // -1: not yet read from the environment
+int xlin_mode(int mode) {
+  if (mode >= 0) g_wgrad_xlin = mode;
+  if (g_wgrad_xlin < 0) {
+    const char* e = getenv("SIMCLR_WGRAD_XLIN");
+    g_wgrad_xlin = e ? atoi(e) : 0;
+  }
+  return g_wgrad_xlin;
+}
+inline uint32_t wgrad_x_linear(const WgradArgs& a) {
+  const int mode = xlin_mode(-1);
+  if (mode == 0 || (mode == 3 && a.K == a.C)) return 0;
+  const int ohw = a.OH * a.OW;
+  if (a.KW == 1 && a.K == a.C && a.ish == 1 && a.isw == 1 && a.ih0 == 0 && a.iw0 == 0 &&
+      a.IH == a.OH && a.IW == a.OW)
+    return (uint32_t)(64 * a.C * 2);  // X row m is output row m
+  if (ohw > 0 && 64 % ohw == 0)
+    return (uint32_t)((size_t)(64 / ohw) * a.IH * a.IW * a.C * 2);  // n advances, (oh, ow) kept
+  return 0;
+}
+
 template <int BCO, int BKK, int WM, int WN, int MF>
 void launch_wgrad_xp(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
@@ -2757,7 +2814,12 @@ void launch_wgrad_xp(const WgradArgs& a0, hipStream_t s) {
   a.nKk = (a.K + BKK - 1) / BKK;
   const int grid = a.nCo * a.nKk * a.splits;
   const size_t lds = (size_t)2 * 64 * (BCO + BKK) * 2;
-  hipLaunchKernelGGL((wgrad_xp<BCO, BKK, WM, WN, MF>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
+  a.x_step = wgrad_x_linear(a);
+  if (a.x_step != 0)
+    hipLaunchKernelGGL((wgrad_xp<BCO, BKK, WM, WN, MF, true>), dim3(grid), dim3(64 * WM * WN), lds,
+                       s, a);
+  else
+    hipLaunchKernelGGL((wgrad_xp<BCO, BKK, WM, WN, MF>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
   HIP_CHECK_LAUNCH();
 }
 
@@ -2810,7 +2872,8 @@ constexpr int WG_VARIANTS[][3] = {{128, 128, 768}, {64, 128, 768}, {128, 64, 768
                                   {64, 128, 768}, {128, 64, 768},
                                   {256, 256, 256}, {256, 128, 256}, {128, 256, 256},
                                   {256, 256, 256},
-                                  {256, 256, 256}, {256, 128, 256}, {128, 128, 512}};
+                                  {256, 256, 256}, {256, 128, 256}, {128, 128, 512},
+                                  {256, 256, 256}};
 constexpr int WG_GLDS0 = 6;
 constexpr int WG_PATCH0 = 17;  // wgrad_patch (3x3 stride-1, all taps from one input patch)
 // wgrad_tn with loads two steps ahead (DEEP): the 64 x 128 / 128 x 64 tiles gain 10-17 % on the
@@ -2825,6 +2888,12 @@ constexpr int WG_PIPE0 = 20;
 constexpr int WG_GLDS32 = 23;
 // 24-26: wgrad_xp (fragment reads carried across the barrier, no prologues) on 32x32x16:
 // 256 x 256 / 256 x 128 (8 waves), 128 x 128 (4 waves)
+// 27: wgrad_xp 256 x 256 on 4 waves (128 x 128 per wave, one wave per SIMD): per 64-row step the
+// 8-wave tile reads 196 KB of LDS fragments + 64 KB of DMA writes against ~2,060 MFMA clocks per
+// SIMD (LDS at parity with the MFMAs, 128 B/clk); the 128 x 128 wave tile reads 128 KB (LDS at
+// ~75 % of the MFMA time).  The 256 accumulator registers per lane live in AGPRs.  Measured
+// 15-20 % slower than 24 on every shape (one wave per SIMD: its own VALU address work and DMA
+// issue sit between its MFMAs; profiles/r6_wgrad_pmc.md); kept for the record and the sweep.
 constexpr int WG_XP0 = 24;
 
 
@@ -3482,6 +3551,7 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
 
 
 int wgrad_num_variants() { return (int)(sizeof(WG_VARIANTS) / sizeof(WG_VARIANTS[0])); }
+int wgrad_xlin(int mode) { return xlin_mode(mode); }
 int wgrad_default_variant(int N) { return N <= 64 ? 1 : 0; }
 bool wgrad_variant_glds(int v) { return (v >= WG_GLDS0 && v < WG_PATCH0) || v >= WG_PIPE0; }
 int wgrad_variant_area(int v) { return WG_VARIANTS[v][0] * WG_VARIANTS[v][1]; }
@@ -3613,6 +3683,7 @@ void conv_wgrad(const ConvGeom& g, const uint16_t* dY, const uint16_t* X, size_t
     case 24: launch_wgrad_xp<256, 256, 2, 4, 32>(a, s); break;
     case 25: launch_wgrad_xp<256, 128, 4, 2, 32>(a, s); break;
     case 26: launch_wgrad_xp<128, 128, 2, 2, 32>(a, s); break;
+    case 27: launch_wgrad_xp<256, 256, 2, 2, 32>(a, s); break;
     case 0: launch_wgrad<128, 128, 2, 2>(a, s); break;
     case 1: launch_wgrad<64, 128, 2, 2>(a, s); break;
     case 2: launch_wgrad<128, 64, 2, 2>(a, s); break;

@@ -71,6 +71,8 @@ void conv_igemm_nt(const ConvGeom& g, const uint16_t* A, size_t a_elems, const u
                    uint16_t* out, const float* bias, float* stats, const ConvFusion& f,
                    int variant, hipStream_t s);
 int wgrad_num_variants();
+// wgrad_xp's step-affine X addressing: set the mode (>= 0) and/or return it (SIMCLR_WGRAD_XLIN)
+int wgrad_xlin(int mode);
 int wgrad_default_variant(int N);
 bool wgrad_variant_glds(int v);  // LDS-DMA variant (see wgrad_variant_ok)
 int wgrad_variant_area(int v);   // output tile elements (BCO x BKK)

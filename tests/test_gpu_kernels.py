@@ -485,10 +485,14 @@ def test_igemm_glds_variants(ops, k, s, p, C, Co, H):
                                            (3, 2, 1, 128, 192, 16), (1, 2, 0, 128, 128, 16),
                                            (3, 1, 1, 256, 512, 4), (3, 1, 1, 64, 64, 5),
                                            (3, 1, 1, 64, 64, 32), (3, 1, 1, 128, 128, 16),
-                                           (3, 1, 1, 128, 64, 32)])
-def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
+                                           (3, 1, 1, 128, 64, 32), (3, 1, 1, 64, 128, 8),
+                                           (3, 2, 1, 64, 64, 8)])
+@pytest.mark.parametrize("xlin", [0, 1])
+def test_wgrad_glds_variants(ops, k, s, p, C, Co, H, xlin):
     """LDS-DMA weight gradient (wgrad_glds), every tile variant and a few split counts, against
-    torch's fp32 conv2d weight gradient (partial M tiles: H=5 gives M % 64 != 0)."""
+    torch's fp32 conv2d weight gradient (partial M tiles: H=5 gives M % 64 != 0).  The 1x1
+    stride-1 cases and the ones with OH * OW dividing 64 (8x8, 4x4 outputs) run wgrad_xp's
+    step-affine X addressing (XLIN)."""
     from simclr_amd.ops.conv_hip import fwd_geom
     torch.manual_seed(13)
     N = 8
@@ -505,13 +509,18 @@ def test_wgrad_glds_variants(ops, k, s, p, C, Co, H):
     vs = [v for v in range(ops.wgrad_nvariants())
           if ops.wgrad_variant_glds(v) and ops.wgrad_variant_ok(v, g, False, False)]
     assert vs
-    for v in vs:
-        base = ops.wgrad_splits(g, v)
-        for splits in sorted({1, 3, base}):
-            part = torch.empty(splits * Co * K, device=DEV)
-            out = torch.empty(Co, k, k, C, device=DEV)
-            ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, None, None, 0, False, 1, v)
-            assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)
+    prev = ops.wgrad_xlin(-1)
+    assert ops.wgrad_xlin(xlin) == xlin
+    try:
+        for v in vs:
+            base = ops.wgrad_splits(g, v)
+            for splits in sorted({1, 3, base}):
+                part = torch.empty(splits * Co * K, device=DEV)
+                out = torch.empty(Co, k, k, C, device=DEV)
+                ops.wgrad(dyn, xn, part, out, g, splits, C, 0.0, None, None, 0, False, 1, v)
+                assert _rel(out.permute(0, 3, 1, 2), wr.grad) < 1e-2, (v, splits)
+    finally:
+        ops.wgrad_xlin(prev)
 
 
 @pytest.mark.parametrize("k,p,C,Co,H", [(3, 1, 128, 128, 16), (3, 1, 64, 128, 32),

@@ -97,7 +97,7 @@ def main():
         f"experiment.base_cnn={a.model}", f"model.cifar_stem={'true' if a.cifar_stem else 'null'}",
         f"experiment.batches={a.batch}", "data.synthetic=true", "parameter.epochs=10"]))
     tr = Trainer(cfg, st, 50000)
-    loader = ContrastiveLoader(synthetic_dataset(max(2048, 4 * a.batch), 10, size=a.size), a.batch,
+    loader = ContrastiveLoader(synthetic_dataset(max(2048, (3 + a.steps) * a.batch), 10, size=a.size), a.batch,
                                dev, seed=7)
     it = iter(loader)
     for _ in range(2):  # warm-up + autotune
