@@ -959,6 +959,18 @@ void maxpool_bwd_op(const Tensor& dy, const Tensor& arg, const Tensor& dx, int64
               (int)S, (int)P, cur_stream());
 }
 
+// ImageNet stem: 2x2 space-to-depth of the zero-padded image (7x7/s2 -> 4x4/s1 conv)
+void stem_s2d_op(const Tensor& img, int64_t creal, int64_t P, const Tensor& xs) {
+  TORCH_CHECK(img.dim() == 4 && xs.dim() == 4, "stem_s2d: NHWC 4-D");
+  const int Nb = img.size(0), H = img.size(1), W = img.size(2), Cin = img.size(3);
+  TORCH_CHECK(Cin % 4 == 0 && creal >= 1 && creal <= 4 && P >= 0, "stem_s2d: channels / pad");
+  TORCH_CHECK((H + 2 * P) % 2 == 0 && (W + 2 * P) % 2 == 0, "stem_s2d: padded size must be even");
+  TORCH_CHECK(xs.size(0) == Nb && xs.size(1) == (H + 2 * P) / 2 && xs.size(2) == (W + 2 * P) / 2 &&
+                  xs.size(3) == 16, "stem_s2d: output shape");
+  stem_s2d(bf(img, "img"), bfw(xs, "xs"), Nb, H, W, Cin, (int)creal, (int)xs.size(1),
+           (int)xs.size(2), (int)P, cur_stream());
+}
+
 // pooled ImageNet stem: BN + ReLU + max-pool forward, max-pool + ReLU-mask + BN backward
 void bn_relu_maxpool_op(const Tensor& a, const Tensor& ss, int64_t S, const Tensor& y,
                         const Tensor& arg, const Tensor& asel, int64_t K, int64_t Sd, int64_t P) {
@@ -1030,6 +1042,7 @@ void class_sums_op(const Tensor& X, const Tensor& y, int64_t NC, const Tensor& s
 TORCH_LIBRARY(simclr_amd, m) {
   m.def("maxpool_fwd(Tensor x, Tensor(a!) y, Tensor(b!) arg, int K, int S, int P) -> ()", &maxpool_fwd_op);
   m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
+  m.def("stem_s2d(Tensor img, int creal, int P, Tensor(a!) xs) -> ()", &stem_s2d_op);
   m.def("bn_relu_maxpool(Tensor a, Tensor ss, int S, Tensor(a!) y, Tensor(b!) arg, Tensor(c!) asel, "
         "int K, int Sd, int P) -> ()", &bn_relu_maxpool_op);
   m.def("maxpool_bwd_bn(Tensor gy, Tensor arg, Tensor y, Tensor a, Tensor coef, int S, Tensor(a!) da, "

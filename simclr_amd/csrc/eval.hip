@@ -101,6 +101,47 @@ __global__ void k_maxpool_bwd(const uint16_t* __restrict__ dy, const uint8_t* __
   }
 }
 
+// 2x2 space-to-depth of the zero-padded image for the ImageNet stem: a 7x7 / stride-2 / pad-P
+// convolution over C <= 4 channels equals a 4x4 / stride-1 / unpadded one over
+// xs[n][i][j][(dy * 2 + dx) * 4 + c] = img[n][2i + dy - P][2j + dx - P][c] (zero outside the
+// image and for c >= creal) with the kernel folded the same way (models/fused.py _s2d_weight).
+// K = 256 instead of 49 taps x 8 gathered channels = 392, every gather 32 contiguous bytes instead
+// of 16 (tools/stem_s2d_probe.py: forward 1310 -> 889 us, weight gradient 1621 -> 858 us at
+// 224x224, batch 1024).  One thread per (n, i, j, dy): two input pixels in, 16 bytes out.
+__global__ void k_stem_s2d(const uint16_t* __restrict__ img, uint16_t* __restrict__ xs, int Nb,
+                           int H, int W, int Cin, int creal, int HS, int WS, int P) {
+  const size_t total = (size_t)Nb * HS * WS * 2;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int dy = (int)(t & 1);
+    const size_t pix = t >> 1;
+    const int j = (int)(pix % WS);
+    const size_t r = pix / WS;
+    const int i = (int)(r % HS);
+    const int n = (int)(r / HS);
+    const int ih = 2 * i + dy - P;
+    uint16_t v[8];
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int iw = 2 * j + dx - P;
+      uint2 q = make_uint2(0u, 0u);
+      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        q = *reinterpret_cast<const uint2*>(img + (((size_t)n * H + ih) * W + iw) * Cin);
+      v[dx * 4 + 0] = (uint16_t)(q.x & 0xffffu);
+      v[dx * 4 + 1] = creal > 1 ? (uint16_t)(q.x >> 16) : 0;
+      v[dx * 4 + 2] = creal > 2 ? (uint16_t)(q.y & 0xffffu) : 0;
+      v[dx * 4 + 3] = creal > 3 ? (uint16_t)(q.y >> 16) : 0;
+    }
+    uint4 o;
+    o.x = v[0] | ((uint32_t)v[1] << 16);
+    o.y = v[2] | ((uint32_t)v[3] << 16);
+    o.z = v[4] | ((uint32_t)v[5] << 16);
+    o.w = v[6] | ((uint32_t)v[7] << 16);
+    *reinterpret_cast<uint4*>(xs + pix * 16 + dy * 8) = o;
+  }
+}
+
+
 // ---------------------------------------------------------------------------- pooled stem
 // The ImageNet-shape stem (reference model.py:90-92 keeps torchvision's 7x7/s2 conv -> BN ->
 // ReLU -> MaxPool2d(3, 2, 1) for resnet50), fused around the max-pool:
@@ -358,6 +399,13 @@ void bn_relu_maxpool(const uint16_t* a, const float* ss, int S, uint16_t* y, uin
                      int P, hipStream_t s) {
   hipLaunchKernelGGL(k_bn_relu_maxpool, dim3(grid_cap((size_t)Nb * OH * OW * (C / 8))), dim3(256),
                      0, s, a, ss, S, y, arg, asel, Nb, H, W, C, OH, OW, K, Sd, P);
+  HIP_CHECK_LAUNCH();
+}
+
+void stem_s2d(const uint16_t* img, uint16_t* xs, int Nb, int H, int W, int Cin, int creal,
+              int HS, int WS, int P, hipStream_t s) {
+  hipLaunchKernelGGL(k_stem_s2d, dim3(grid_cap((size_t)Nb * HS * WS * 2)), dim3(256), 0, s, img,
+                     xs, Nb, H, W, Cin, creal, HS, WS, P);
   HIP_CHECK_LAUNCH();
 }
 

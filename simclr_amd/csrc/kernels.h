@@ -238,6 +238,9 @@ void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int Nb, int H, in
                  int OH, int OW, int K, int S, int P, hipStream_t s);
 void maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int Nb, int H, int W,
                  int C, int OH, int OW, int K, int S, int P, hipStream_t s);
+// ImageNet stem as a 4x4 stride-1 conv: 2x2 space-to-depth of the P-padded image (C <= 4 real)
+void stem_s2d(const uint16_t* img, uint16_t* xs, int Nb, int H, int W, int Cin, int creal,
+              int HS, int WS, int P, hipStream_t s);
 void bn_relu_maxpool(const uint16_t* a, const float* ss, int S, uint16_t* y, uint8_t* arg,
                      uint16_t* asel, int Nb, int H, int W, int C, int OH, int OW, int K, int Sd,
                      int P, hipStream_t s);

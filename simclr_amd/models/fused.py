@@ -213,6 +213,10 @@ class FusedStages:
         # (serial, ~10 µs at the full chip) instead of the weight-gradient stream
         self.dual_reduce_main = False
         self.fused_ds_dual = True
+        # the ImageNet stem (7x7 / stride 2 / pad 3 over the 3 image channels) as a 4x4 / stride-1
+        # conv over the 2x2 space-to-depth of the padded image (csrc/eval.hip k_stem_s2d):
+        # K 256 instead of 392 gathered columns, 32-byte instead of 16-byte gathers
+        self.stem_s2d = True
         # ... and layer2.0's stride-2 downsample (Co 512 / Ci 256, dY materialised): measured
         # neutral to +0.06 ms (r6 log), so off by default
         self.fused_ds_dual_s2 = False
@@ -337,6 +341,44 @@ class FusedStages:
         rows_seg = a.shape[0] * a.shape[1] * a.shape[2] // S
         return a, self._bn_fwd(ops, cs.bn, partial, nblk, rows_seg, S, st, slot=slot)
 
+    def _s2d_ok(self, cs: _ConvSpec, xn: torch.Tensor) -> bool:
+        """The stem conv runs in its space-to-depth form (``stem_s2d``)."""
+        if not (getattr(self, "stem_s2d", False) and cs is self.stem and xn.is_cuda):
+            return False
+        Nb, H, W, C = xn.shape
+        return (cs.k == 7 and cs.stride == 2 and cs.pad == 3 and cs.conv.in_channels <= 4
+                and C % 4 == 0 and (H + 6) % 2 == 0 and (W + 6) % 2 == 0)
+
+    def _s2d_input(self, ops, xn: torch.Tensor) -> torch.Tensor:
+        """[Nb, (H+6)/2, (W+6)/2, 16]: the padded image, 2x2 space-to-depth (kept for the
+        weight gradient of the same step)."""
+        c = getattr(self, "_s2d_cache", None)
+        if c is not None and c[0] is xn:
+            return c[1]
+        Nb, H, W, _ = xn.shape
+        xs = _empty_nhwc(Nb, (H + 6) // 2, (W + 6) // 2, 16, xn.device)
+        ops.stem_s2d(xn, self.stem.conv.in_channels, 3, xs)
+        self._s2d_cache = (xn, xs)
+        return xs
+
+    @staticmethod
+    def _s2d_weight(weight: torch.Tensor) -> torch.Tensor:
+        """7x7 kernel [Co][Ci<=4][7][7] -> the 4x4 kernel over the space-to-depth input,
+        OHWI [Co][4][4][16]: w'[co][bh][bw][(dy * 2 + dx) * 4 + c] = w[co][c][2bh + dy][2bw + dx]
+        (zero at 2bh + dy = 7 or 2bw + dx = 7 and for c >= Ci)."""
+        w = shadow_ohwi(weight, weight.shape[1])  # [Co][7][7][Ci] bf16
+        Co, Ci = w.shape[0], w.shape[-1]
+        w8 = torch.nn.functional.pad(w, (0, 4 - Ci, 0, 1, 0, 1))  # [Co][8][8][4]
+        return w8.view(Co, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(Co, 4, 4, 16)
+
+    @staticmethod
+    def _s2d_unfold_grad(gs: torch.Tensor, out: torch.Tensor) -> None:
+        """Weight gradient of the 4x4 form [Co][4][4][16] -> the 7x7 kernel's, OHWI
+        [Co][7][7][Ci] (``out``, fp32)."""
+        Co, Ci = out.shape[0], out.numel() // (out.shape[0] * 49)
+        g8 = gs.view(Co, 4, 4, 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(Co, 8, 8, 4)
+        out.view(Co, 7, 7, Ci).copy_(g8[:, :7, :7, :Ci])
+
     def _conv_fwd(self, ops, xn, cs: _ConvSpec, pro_ss: Optional[torch.Tensor], S: int,
                   dual=None):
         """a = conv(pro(x)) with BN statistics partials in the epilogue.
@@ -350,9 +392,14 @@ class FusedStages:
         Co = cs.conv.out_channels
         OH = (H + 2 * cs.pad - cs.k) // cs.stride + 1
         OW = (W + 2 * cs.pad - cs.k) // cs.stride + 1
-        w = shadow_ohwi(cs.conv.weight, C)
         a = _empty_nhwc(Nb, OH, OW, Co, xn.device)
-        g = fwd_geom(Nb, H, W, C, OH, OW, cs.k, cs.k, cs.stride, cs.pad, Co)
+        if dual is None and pro_ss is None and self._s2d_ok(cs, xn):
+            xn = self._s2d_input(ops, xn)
+            w = self._s2d_weight(cs.conv.weight)
+            g = fwd_geom(Nb, xn.shape[1], xn.shape[2], 16, OH, OW, 4, 4, 1, 0, Co)
+        else:
+            w = shadow_ohwi(cs.conv.weight, C)
+            g = fwd_geom(Nb, H, W, C, OH, OW, cs.k, cs.k, cs.stride, cs.pad, Co)
         M = Nb * OH * OW
         pro, dl, A = None, None, xn
         if dual is not None:
@@ -483,7 +530,12 @@ class FusedStages:
         Nb, H, W, C = xn.shape
         Co = cs.conv.out_channels
         OH, OW = dyn.shape[1], dyn.shape[2]
-        g = fwd_geom(Nb, H, W, C, OH, OW, cs.k, cs.k, cs.stride, cs.pad, Co)
+        s2d = pro_ss is None and self._s2d_ok(cs, xn)
+        if s2d:
+            xn = self._s2d_input(ops, xn)
+            g = fwd_geom(Nb, xn.shape[1], xn.shape[2], 16, OH, OW, 4, 4, 1, 0, Co)
+        else:
+            g = fwd_geom(Nb, H, W, C, OH, OW, cs.k, cs.k, cs.stride, cs.pad, Co)
         M = Nb * OH * OW
         pro = None
         if pro_ss is not None:
@@ -496,6 +548,13 @@ class FusedStages:
         def run():
             if _SKIP_WGRAD:  # attribution experiment only: the step without weight gradients
                 _deliver_grad(cs.conv.weight, lambda out: None)
+                return
+            if s2d:  # the 4x4 form's gradient, folded back onto the 7x7 kernel
+                def s2d_grad(out):
+                    gs = torch.empty((Co, 4, 4, 16), device=dyn.device, dtype=torch.float32)
+                    run_wgrad(ops, dyn, xn, gs, g, 16, pro=pro, dpro=dpro, concurrent=concurrent)
+                    self._s2d_unfold_grad(gs, out)
+                _deliver_grad(cs.conv.weight, s2d_grad)
                 return
             # creal: the stem's 3 image channels are gathered as 8 (zero-padded)
             _deliver_grad(cs.conv.weight,

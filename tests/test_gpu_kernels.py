@@ -627,6 +627,19 @@ def test_wgrad_bn_backward_prologue_padded_channels(ops, k, s, p, H):
     assert checked >= len(vs)
 
 
+@pytest.mark.parametrize("N,H,creal", [(2, 224, 3), (4, 32, 3), (3, 30, 2)])
+def test_stem_s2d_kernel(ops, N, H, creal):
+    """k_stem_s2d: the padded image's 2x2 space-to-depth, bitwise equal to the torch reshuffle
+    (channels >= creal zeroed even where the image holds garbage there)."""
+    from test_stem_s2d import s2d_reference
+    torch.manual_seed(5)
+    img = _bf(torch.randn(N, H, H, 8, device=DEV))
+    xs = torch.full((N, (H + 6) // 2, (H + 6) // 2, 16), 7.0, device=DEV, dtype=torch.bfloat16)
+    ops.stem_s2d(img, creal, 3, xs)
+    torch.cuda.synchronize()
+    assert torch.equal(xs, s2d_reference(img, creal))
+
+
 @pytest.mark.parametrize("N,H,C", [(4, 16, 64), (6, 17, 64), (2, 112, 64)])
 def test_pooled_stem_kernels(ops, N, H, C):
     """The ImageNet stem's fused BN + ReLU + MaxPool2d(3, 2, 1) forward (bn_relu_maxpool) and
