@@ -213,6 +213,10 @@ class FusedStages:
         # (serial, ~10 µs at the full chip) instead of the weight-gradient stream
         self.dual_reduce_main = False
         self.fused_ds_dual = True
+        # persistent blocks per view segment of the fused 1x1 backward kernels (A/B knobs):
+        # narrow form / layer1.0 downsample, and the wide form (x 2 Ci slices)
+        self.bwd1x1_bps = _BWD1X1_BPS
+        self.bwd1x1_bps_wide = 64
         # the ImageNet stem (7x7 / stride 2 / pad 3 over the 3 image channels) as a 4x4 / stride-1
         # conv over the 2x2 space-to-depth of the padded image (csrc/eval.hip k_stem_s2d):
         # K 256 instead of 392 gathered columns, 32-byte instead of 16-byte gathers
@@ -607,7 +611,7 @@ class FusedStages:
         wide = (Co, Ci) == (512, 128)
         # the wide kernel launches 2 blocks (Ci slices) per row block: 64 row blocks per view
         # segment fill the chip's 256 CUs once at S = 2
-        bps = self._bwd1x1_bps(M // S, 64 if wide else _BWD1X1_BPS)
+        bps = self._bwd1x1_bps(M // S, self.bwd1x1_bps_wide if wide else self.bwd1x1_bps)
         xraw = xin if (wide and xin is not None and xin is not a_prev) else None
         w = shadow_ohwi(cs.conv.weight, Ci)
         wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
@@ -688,7 +692,7 @@ class FusedStages:
             ops.conv1x1_bwd_dual_s2(dad, None, None, tp.x, wt, resid, wpart, S, bps)
         else:
             M = Nb * H * W
-            bps = self._bwd1x1_bps(M // S)
+            bps = self._bwd1x1_bps(M // S, self.bwd1x1_bps)
             w = shadow_ohwi(cs.conv.weight, Ci)
             wt = self._dgrad_weight(ops, cs, w, (0, 0), [Co, 1, 1, Ci, 1, 1, 0, -1, 0, -1])
             resid = _empty_nhwc(Nb, H, W, Ci, dev)
