@@ -3195,8 +3195,13 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* Ds = (uint16_t*)smem;          // [2][32][CO]  tr_swz<CO> image of dY
   uint16_t* Xs = Ds + 2 * BMT * CO;        // [2][32][CI]  tr_swz<CI> image of relu(bn2(a2)) (slice)
-  uint16_t* Xr = Xs + 2 * BMT * CI;        // [2][32][CI]  raw a2 (slice)
-  uint16_t* Ws = Xr + 2 * BMT * CI;        // [CI][CO]     Wᵀ slice, chunk ^= row & 7
+  // Xr rows padded to XRS = CI + 8 elements (144 bytes): the epilogue's 8-byte reads of 16
+  // consecutive rows at one column then hit 16 distinct bank pairs (at 128-byte rows they
+  // were 8-way conflicts).  Ws chunks are XORed with row & 15: the dgrad's 16-row b128 reads
+  // of one chunk column land on 16 distinct chunks (row & 7 left them 2-way)
+  constexpr int XRS = CI + 8;
+  uint16_t* Xr = Xs + 2 * BMT * CI;        // [2][32][XRS] raw a2 (slice)
+  uint16_t* Ws = Xr + 2 * BMT * XRS;       // [CI][CO]     Wᵀ slice, chunk ^= row & 15
   float* red = (float*)(Ws + CI * CO);     // [RG row groups][CI][2]
   float* Tb = red + RG * CI * 2;           // [4][CI]  BN2 scale, shift, mean, invstd (slice)
   float* Cf = Tb + 4 * CI;                 // [3][CO]  BN3-backward A, B, D (LAZY)
@@ -3223,7 +3228,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
 
   for (int c = tid; c < CI * CO / 8; c += NT) {
     const int row = c / (CO / 8), ch = c % (CO / 8);
-    *(u32x4*)(Ws + row * CO + ((ch ^ (row & 7)) * 8)) =
+    *(u32x4*)(Ws + row * CO + ((ch ^ (row & 15)) * 8)) =
         *(const u32x4*)(p.Wt + ((size_t)(c0 + row) * CO + ch * 8));
   }
   for (int i = tid; i < (PLAIN ? 0 : 4 * CI); i += NT) {
@@ -3288,9 +3293,9 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
     if (xown) {
       *(u32x4*)(Xs + buf * BMT * CI + xrow * CI + tr_swz<CI>(xrow, xch * 8)) =
           (XPRE || PLAIN) ? X1 : affine_relu8(X1, Tb + xch * 8, Tb + CI + xch * 8, true, true);
-      if (!XPRE && !PLAIN) *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
+      if (!XPRE && !PLAIN) *(u32x4*)(Xr + buf * BMT * XRS + xrow * XRS + xch * 8) = X1;
     } else if (XPRE && !PLAIN) {
-      *(u32x4*)(Xr + buf * BMT * CI + xrow * CI + xch * 8) = X1;
+      *(u32x4*)(Xr + buf * BMT * XRS + xrow * XRS + xch * 8) = X1;
     }
   };
 
@@ -3319,7 +3324,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
 #pragma unroll
       for (int fn = 0; fn < NF; ++fn) {
         const int wr = cq * CW + fn * 16 + li;
-        const bf16x8 af = *(const bf16x8*)(Ws + wr * CO + ((lch ^ (wr & 7)) * 8));
+        const bf16x8 af = *(const bf16x8*)(Ws + wr * CO + ((lch ^ (wr & 15)) * 8));
         accd[fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, accd[fn], 0, 0, 0);
       }
     }
@@ -3332,7 +3337,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1_bwd_dual_w(Dual1x1Args p) {
       const u32x2 w = {pack2bf(accd[fn][0], accd[fn][1]), pack2bf(accd[fn][2], accd[fn][3])};
       __builtin_nontemporal_store(w, (u32x2*)(p.gm + (size_t)m * CIT + c0 + ci));
     } else {
-    const uint16_t* xr = Xr + cur * BMT * CI + mrow * CI;
+    const uint16_t* xr = Xr + cur * BMT * XRS + mrow * XRS;
     const u32x2 yv = *(const u32x2*)(xr + ci);
     const float4 tsc = *(const float4*)(Tb + ci), tsh = *(const float4*)(Tb + CI + ci);
     const float4 tmu = *(const float4*)(Tb + 2 * CI + ci);
@@ -3761,7 +3766,7 @@ size_t conv1x1_bwd_dual_lds() {
 }
 
 size_t conv1x1_bwd_dual_w_lds(int CO, int BMT = 32) {
-  return (size_t)2 * BMT * CO * 2 + (size_t)2 * 2 * BMT * 64 * 2 + (size_t)64 * CO * 2 +
+  return (size_t)2 * BMT * CO * 2 + (size_t)2 * BMT * (64 + 72) * 2 + (size_t)64 * CO * 2 +
          (size_t)(BMT / 16) * 64 * 2 * 4 + (size_t)4 * 64 * 4 + (size_t)3 * CO * 4;
 }
 
