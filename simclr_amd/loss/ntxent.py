@@ -66,6 +66,22 @@ def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
     return _SIDE[dev]
 
 
+# z all-gathers the fused projection head already issued on the side stream, one per view, each
+# under the next view's GEMM 2 (models/head_fused.py): (device, z.data_ptr()) -> (zb_all,
+# tensors the side stream still uses).  The loss takes the gathered rows from here instead of
+# issuing its own all-gather.
+_PREGATHER: dict = {}
+
+
+def register_pregather(z: torch.Tensor, zb_all: torch.Tensor, keep) -> None:
+    _PREGATHER.clear()  # one step in flight per process
+    _PREGATHER[(z.device, z.data_ptr())] = (zb_all, keep)
+
+
+def take_pregather(z: torch.Tensor):
+    return _PREGATHER.pop((z.device, z.data_ptr()), None)
+
+
 class _NTXentHipFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, n, temperature, reduction, gather, st):
@@ -90,13 +106,19 @@ class _NTXentHipFn(torch.autograd.Function):
             cur = torch.cuda.current_stream(dev)
             side = _side_stream(dev)
             side.wait_stream(cur)
-            zb_all = torch.empty((Ccols, D), device=dev, dtype=torch.bfloat16)
-            with torch.cuda.stream(side):
-                ipc = getattr(st, "ipc", None)
-                if ipc is not None:  # one-shot stores over xGMI (comm/ipc.py, csrc/comm.hip)
-                    ipc.all_gather(("ntxent", "z"), zb, zb_all)
-                else:
-                    dist.all_gather_into_tensor(zb_all, zb, group=st.group)
+            pre = take_pregather(zb)
+            if pre is not None and tuple(pre[0].shape) == (Ccols, D):
+                # the head gathered z view by view on this side stream, under its GEMM 2
+                zb_all, pre_keep = pre
+            else:
+                pre_keep = None
+                zb_all = torch.empty((Ccols, D), device=dev, dtype=torch.bfloat16)
+                with torch.cuda.stream(side):
+                    ipc = getattr(st, "ipc", None)
+                    if ipc is not None:  # one-shot stores over xGMI (comm/ipc.py, csrc/comm.hip)
+                        ipc.all_gather(("ntxent", "z"), zb, zb_all)
+                    else:
+                        dist.all_gather_into_tensor(zb_all, zb, group=st.group)
             zall = torch.empty((Ccols, D), device=dev, dtype=torch.float32)
             inv_all = torch.empty((Ccols,), device=dev, dtype=torch.float32)
             zn = zall[col_offset:col_offset + R]
@@ -111,6 +133,7 @@ class _NTXentHipFn(torch.autograd.Function):
                                  s_loc, 0)  # overlaps the exchange
             cur.wait_stream(side)
             zb_all.record_stream(cur)
+            del pre_keep  # (the head's per-view gather buffers: the side stream is joined)
             # every row in one launch each (this rank's block is rewritten with identical
             # values, after the local scoring read it: same stream)
             ops.nt_normalize(zb_all, zall, inv_all)

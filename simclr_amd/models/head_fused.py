@@ -106,6 +106,55 @@ def eligible(mod, x: torch.Tensor, segments: int) -> bool:
             and D % 64 == 0 and s.linear1.bias is not None and s.linear2.in_features == H)
 
 
+def _pregather_ok(mod, st, S: int, seg: int, D: int) -> bool:
+    """The NT-Xent with global negatives follows (``mod._zgather``, set by the trainer), over
+    RCCL (the IPC exchange keeps its own one-shot gather in the loss), with one view per
+    segment, and ``SIMCLR_ZGATHER_OVERLAP=1``.  Off by default, measured: GEMM 2 has only
+    16-32 blocks and is bound by its 2,048-deep K loop, so each per-view launch takes as long
+    as the one-launch GEMM 2 (39.4 vs 40 us): the split adds ~40 us to the critical path,
+    more than the 256 KiB z exchange it hides (profiles/r6_optimization_log.md)."""
+    import os
+    return (getattr(mod, "_zgather", False) and st.comm and getattr(st, "ipc", None) is None
+            and S == 2 and D in (32, 64, 128, 256) and (2 * seg) % 16 == 0
+            and os.environ.get("SIMCLR_ZGATHER_OVERLAP", "0") == "1")
+
+
+PREGATHER_CALLS = [0]  # launches of the per-view gather path (tests)
+
+
+def _gemm2_pregather(ops, st, y1, W2, z, v2, bias2, bs, S: int, seg: int, H: int, D: int):
+    """GEMM 2 view by view, each view's z all-gathered over RCCL on the loss's side stream
+    while the next view's GEMM 2 runs (the north star's gather under the projection head).
+    Same tile variant and per-row math as the one-launch GEMM 2, so z is bitwise the same; the
+    gathered rows are assembled rank-major ([rank][view][row]), the layout the loss's
+    one-shot all-gather produces, so the loss is bitwise the same too."""
+    import torch.distributed as dist
+    from ..loss import ntxent as ntx
+    dev = z.device
+    W = st.world_size
+    cur = torch.cuda.current_stream(dev)
+    side = ntx._side_stream(dev)
+    parts = []
+    for v in range(S):
+        rows = slice(v * seg, (v + 1) * seg)
+        zv = z[rows]
+        pro = (bs.ss[0][v * H:(v + 1) * H], bs.ss[1][v * H:(v + 1) * H], seg, True)
+        igemm_launch(ops, y1[rows], W2, zv, _geom(seg, H, D), v2, bias=bias2, pro=pro)
+        tmp = torch.empty((W * seg, D), device=dev, dtype=torch.bfloat16)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            dist.all_gather_into_tensor(tmp, zv, group=st.group)
+        parts.append(tmp)
+    zb_all = torch.empty((W * S * seg, D), device=dev, dtype=torch.bfloat16)
+    with torch.cuda.stream(side):
+        za = zb_all.view(W, S, seg, D)
+        for v in range(S):
+            za[:, v].copy_(parts[v].view(W, seg, D))
+    # every buffer the side stream touches stays referenced until the loss joins it
+    ntx.register_pregather(z, zb_all, (parts, z))
+    PREGATHER_CALLS[0] += 1
+
+
 class MLPHeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, gamma, beta, w2, b2, mod, S):
@@ -134,7 +183,10 @@ class MLPHeadFn(torch.autograd.Function):
         pro = (bs.ss[0], bs.ss[1], seg, True)
         bias2 = b2.detach().float().contiguous() if b2 is not None else None
         v2 = igemm_choose(ops, y1, W2, z, g2, bias=bias2, pro=pro, seg_rows=seg)
-        igemm_launch(ops, y1, W2, z, g2, v2, bias=bias2, pro=pro)
+        if _pregather_ok(mod, st, S, seg, D):
+            _gemm2_pregather(ops, st, y1, W2, z, v2, bias2, bs, S, seg, H, D)
+        else:
+            igemm_launch(ops, y1, W2, z, g2, v2, bias=bias2, pro=pro)
         # the backward's transposed weights, one batched launch (weights are final until the
         # optimizer step, which comes after the backward)
         wt1, wt2 = _transposed(ops, mod, W1, W2, K, H, D)

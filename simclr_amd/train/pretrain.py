@@ -94,6 +94,12 @@ class Trainer:
         self._early_updates()
         self.loss_fn = NTXent(temperature=cfg["parameter"]["temperature"],
                               gather=cfg_get(cfg, "loss.gather", False))
+        # global negatives over RCCL: the fused head gathers z view by view under its GEMM 2
+        # (models/head_fused.py _gemm2_pregather)
+        zg = self.loss_fn.gather is True and bool(st.comm)
+        for m in self.model.modules():
+            if hasattr(m, "use_fused") and hasattr(m, "_seq"):
+                m._zgather = zg
         self.hip = self.device.type == "cuda" and registry.use_hip(self.store.master) \
             and self.precision == "bf16"
         self.model.train()

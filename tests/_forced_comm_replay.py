@@ -94,6 +94,41 @@ def run(st, gather: bool, batch: int, xs) -> dict:
     return res
 
 
+def zgather_overlap(st, dev) -> dict:
+    """Global negatives at a batch the fused head takes (256 rows per view): z all-gathered
+    view by view under the head's GEMM 2 (models/head_fused.py _gemm2_pregather) against the
+    loss's one-shot all-gather, eagerly and as a captured step replayed by the multi-stream
+    executor — losses and fp32 master bitwise equal over 3 steps."""
+    from simclr_amd.data.datasets import synthetic_dataset
+    from simclr_amd.data.loader import ContrastiveLoader
+    from simclr_amd.models import head_fused
+    batch = 256
+    loader = ContrastiveLoader(synthetic_dataset(1024, 10), batch, dev, seed=11)
+    xs = [x.clone() for x, _ in loader][:4]
+    out = {"zgather": True}
+    arms = {}
+    for name, flag in (("oneshot", "0"), ("overlap", "1"), ("overlap_streams", "1")):
+        os.environ["SIMCLR_ZGATHER_OVERLAP"] = flag
+        t = _trainer(st, True, batch)
+        c0 = head_fused.PREGATHER_CALLS[0]
+        t.step(xs[0])  # eager, every arm: the head's weight-transpose plan exists before capture
+        if name == "overlap_streams":
+            t.capture(xs[0], warmup=0)
+            t.replay_mode = "streams"
+        ls = [float(t.step(x).item()) for x in xs[1:]]
+        torch.cuda.synchronize()
+        arms[name] = (ls, t.store.master.detach().clone(), head_fused.PREGATHER_CALLS[0] - c0)
+        if t.sreplay is not None:
+            t.sreplay.close()
+    os.environ.pop("SIMCLR_ZGATHER_OVERLAP", None)
+    ref = arms["oneshot"]
+    out["losses"] = {k: v[0] for k, v in arms.items()}
+    out["pregather_calls"] = {k: v[2] for k, v in arms.items()}
+    out["equal"] = {k: {"loss": v[0] == ref[0], "master": bool(torch.equal(v[1], ref[1]))}
+                    for k, v in arms.items() if k != "oneshot"}
+    return out
+
+
 def main() -> int:
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -114,6 +149,7 @@ def main() -> int:
     xs = [x.clone() for x, _ in loader][:5]
     for gather in (False, True):
         print(json.dumps(run(st, gather, batch, xs)), flush=True)
+    print(json.dumps(zgather_overlap(st, dev)), flush=True)
     dist.destroy_process_group()
     return 0
 

@@ -33,7 +33,18 @@ def test_forced_comm_eager_graph_streams_bitwise():
                        cwd=str(ROOT))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
     res = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    zg = [x for x in res if x.get("zgather")]
+    res = [x for x in res if not x.get("zgather")]
     assert [x["gather"] for x in res] == [False, True], r.stdout[-2000:]
+    # the z all-gather issued view by view under the projection head's GEMM 2 (the north
+    # star's overlap) is bitwise the one-shot gather, eager and replayed
+    assert len(zg) == 1, r.stdout[-2000:]
+    print(json.dumps(zg[0]))
+    assert zg[0]["pregather_calls"]["oneshot"] == 0, zg[0]
+    assert zg[0]["pregather_calls"]["overlap"] >= 3, zg[0]
+    assert zg[0]["pregather_calls"]["overlap_streams"] >= 1, zg[0]
+    for mode, eq in zg[0]["equal"].items():
+        assert all(eq.values()), (mode, eq, zg[0]["losses"])
     for x in res:
         print(json.dumps(x))
         st = x["stream_stats"]
