@@ -5,6 +5,7 @@ dense MFMA load: MI355X guide, 'DVFS give-back').
 Prints one markdown table: hipBLASLt (torch.matmul) bf16 GEMMs on random data at large shapes,
 and this framework's LDS-DMA implicit GEMM (csrc/conv.hip igemm_glds) on the same shapes
 expressed as a 1x1 convolution, best tile variant.  Usage (GPU box): python tools/mfma_ceiling.py
+[MxNxK ...]
 """
 import os
 import sys
@@ -37,8 +38,11 @@ def main():
     torch.manual_seed(0)
     print("| M x N x K | hipBLASLt bf16 TF/s | igemm_glds best TF/s (variant) |")
     print("|---|---:|---:|")
-    for M, N, K in ((8192, 8192, 8192), (16384, 4096, 4096), (65536, 256, 2304),
-                    (262144, 128, 1152), (1048576, 64, 576)):
+    shapes = ((8192, 8192, 8192), (16384, 4096, 4096), (65536, 256, 2304),
+              (262144, 128, 1152), (1048576, 64, 576))
+    if len(sys.argv) > 1:  # e.g. 65536x1024x256 65536x256x1024
+        shapes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]]
+    for M, N, K in shapes:
         a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         b = torch.randn(K, N, device=dev, dtype=torch.bfloat16)
         t = _time(lambda: torch.matmul(a, b))
