@@ -959,6 +959,29 @@ void maxpool_bwd_op(const Tensor& dy, const Tensor& arg, const Tensor& dx, int64
               (int)S, (int)P, cur_stream());
 }
 
+// split-K small-M GEMM (projection head GEMM 2): out = relu(bn(A))·Bᵀ + bias
+void gemm_sk_op(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& sc,
+                const c10::optional<Tensor>& sh, int64_t seg, int64_t KS, const Tensor& part,
+                const c10::optional<Tensor>& bias, const Tensor& out) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && out.dim() == 2, "gemm_sk: 2-D operands");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_sk: shapes");
+  TORCH_CHECK(M % 64 == 0 && N % 64 == 0 && KS >= 1 && K % (KS * 32) == 0 && K / KS <= 512,
+              "gemm_sk: M, N multiples of 64; K / KS a multiple of 32, at most 512");
+  TORCH_CHECK(part.numel() >= KS * M * N, "gemm_sk: partial scratch size");
+  TORCH_CHECK(sc.has_value() == sh.has_value(), "gemm_sk: sc and sh together");
+  if (sc.has_value()) {
+    TORCH_CHECK(seg >= 1 && M % seg == 0, "gemm_sk: row segments");
+    TORCH_CHECK(sc->numel() >= (M / seg) * K && sh->numel() >= (M / seg) * K,
+                "gemm_sk: per-segment scale / shift tables");
+  }
+  if (bias.has_value()) TORCH_CHECK(bias->numel() == N, "gemm_sk: bias size");
+  gemm_sk(bf(A, "A"), bf(B, "B"), sc.has_value() ? f32(*sc, "sc") : nullptr,
+          sh.has_value() ? f32(*sh, "sh") : nullptr, (int)seg, (int)M, (int)N, (int)K, (int)KS,
+          f32w(part, "part"), bias.has_value() ? f32(*bias, "bias") : nullptr, bfw(out, "out"),
+          cur_stream());
+}
+
 // ImageNet stem: 2x2 space-to-depth of the zero-padded image (7x7/s2 -> 4x4/s1 conv)
 void stem_s2d_op(const Tensor& img, int64_t creal, int64_t P, const Tensor& xs) {
   TORCH_CHECK(img.dim() == 4 && xs.dim() == 4, "stem_s2d: NHWC 4-D");
@@ -1043,6 +1066,8 @@ TORCH_LIBRARY(simclr_amd, m) {
   m.def("maxpool_fwd(Tensor x, Tensor(a!) y, Tensor(b!) arg, int K, int S, int P) -> ()", &maxpool_fwd_op);
   m.def("maxpool_bwd(Tensor dy, Tensor arg, Tensor(a!) dx, int K, int S, int P) -> ()", &maxpool_bwd_op);
   m.def("stem_s2d(Tensor img, int creal, int P, Tensor(a!) xs) -> ()", &stem_s2d_op);
+  m.def("gemm_sk(Tensor A, Tensor B, Tensor? sc, Tensor? sh, int seg, int KS, Tensor(a!) part, "
+        "Tensor? bias, Tensor(b!) out) -> ()", &gemm_sk_op);
   m.def("bn_relu_maxpool(Tensor a, Tensor ss, int S, Tensor(a!) y, Tensor(b!) arg, Tensor(c!) asel, "
         "int K, int Sd, int P) -> ()", &bn_relu_maxpool_op);
   m.def("maxpool_bwd_bn(Tensor gy, Tensor arg, Tensor y, Tensor a, Tensor coef, int S, Tensor(a!) da, "

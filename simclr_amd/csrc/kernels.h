@@ -187,6 +187,11 @@ void bn_bwd_apply2(const uint16_t* g, const uint16_t* x1, const float* coef1, ui
 void avgpool_fwd(const uint16_t* x, uint16_t* y, int Nb, int HW, int C, hipStream_t s);
 void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int Nb, int HW, int C, hipStream_t s);
 int colsum_groups(int R);  // workspace = colsum_groups(R) * C floats
+// split-K GEMM for small M: out = f(A)·Bᵀ (+ bias), f = BN + ReLU per (row segment, column)
+// when sc != nullptr; part = [KS][M][N] fp32 scratch (misc.hip)
+void gemm_sk(const uint16_t* A, const uint16_t* B, const float* sc, const float* sh, int seg,
+             int M, int N, int K, int KS, float* part, const float* bias, uint16_t* out,
+             hipStream_t s);
 void colsum_bf16(const uint16_t* x, int R, int C, float* out, float beta, float* ws,
                  hipStream_t s);
 void cast_f32_bf16(const float* x, uint16_t* y, size_t n, hipStream_t s);

@@ -106,6 +106,14 @@ def eligible(mod, x: torch.Tensor, segments: int) -> bool:
             and D % 64 == 0 and s.linear1.bias is not None and s.linear2.in_features == H)
 
 
+def _splitk_ok(M: int, H: int, D: int) -> bool:
+    """GEMM 2 as the split-K kernel: 64-row / 64-column tiles, K / 128 >= 2 splits
+    (``SIMCLR_HEAD_SPLITK=0`` keeps the implicit-GEMM launch, A/B)."""
+    import os
+    return (M % 64 == 0 and D % 64 == 0 and H % 128 == 0 and H >= 256
+            and os.environ.get("SIMCLR_HEAD_SPLITK", "1") != "0")
+
+
 def _pregather_ok(mod, st, S: int, seg: int, D: int) -> bool:
     """The NT-Xent with global negatives follows (``mod._zgather``, set by the trainer), over
     RCCL (the IPC exchange keeps its own one-shot gather in the loss), with one view per
@@ -135,11 +143,18 @@ def _gemm2_pregather(ops, st, y1, W2, z, v2, bias2, bs, S: int, seg: int, H: int
     cur = torch.cuda.current_stream(dev)
     side = ntx._side_stream(dev)
     parts = []
+    splitk = _splitk_ok(S * seg, H, D)
     for v in range(S):
         rows = slice(v * seg, (v + 1) * seg)
         zv = z[rows]
-        pro = (bs.ss[0][v * H:(v + 1) * H], bs.ss[1][v * H:(v + 1) * H], seg, True)
-        igemm_launch(ops, y1[rows], W2, zv, _geom(seg, H, D), v2, bias=bias2, pro=pro)
+        sc, sh = bs.ss[0][v * H:(v + 1) * H], bs.ss[1][v * H:(v + 1) * H]
+        if splitk:  # the one-launch path's split-K kernel, per view: the same bits per row
+            ks = H // 128
+            p2 = torch.empty((ks * seg * D,), device=dev, dtype=torch.float32)
+            ops.gemm_sk(y1[rows], W2.view(D, H), sc, sh, seg, ks, p2, bias2, zv)
+        else:
+            igemm_launch(ops, y1[rows], W2, zv, _geom(seg, H, D), v2, bias=bias2,
+                         pro=(sc, sh, seg, True))
         tmp = torch.empty((W * seg, D), device=dev, dtype=torch.bfloat16)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
@@ -185,6 +200,11 @@ class MLPHeadFn(torch.autograd.Function):
         v2 = igemm_choose(ops, y1, W2, z, g2, bias=bias2, pro=pro, seg_rows=seg)
         if _pregather_ok(mod, st, S, seg, D):
             _gemm2_pregather(ops, st, y1, W2, z, v2, bias2, bs, S, seg, H, D)
+        elif _splitk_ok(M, H, D):
+            # split-K GEMM 2 (misc.hip k_gemm_sk): K / 128 splits, fixed-order reduction
+            ks = H // 128
+            part2 = torch.empty((ks * M * D,), device=dev, dtype=torch.float32)
+            ops.gemm_sk(y1, W2.view(D, H), bs.ss[0], bs.ss[1], seg, ks, part2, bias2, z)
         else:
             igemm_launch(ops, y1, W2, z, g2, v2, bias=bias2, pro=pro)
         # the backward's transposed weights, one batched launch (weights are final until the

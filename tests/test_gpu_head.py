@@ -122,9 +122,9 @@ def _head_kernels(m, x, R, S, fused):
 def test_fused_head_cuts_launches():
     """The fused head (K6) issues at most 60 % of the kernels of the per-op head path for the
     same forward + backward (bound to a flat parameter store, as in training).  Measured on
-    MI355X: 9 vs 17 (forward: GEMM, finalize, GEMM, one batched weight transpose; backward:
-    dgrad + mask/partials, one-split weight gradient, finalize, dgrad with the BN-backward
-    prologue, one-split weight gradient)."""
+    MI355X: 10 vs 17 (forward: GEMM, finalize, split-K GEMM + its ordered reduction, one
+    batched weight transpose; backward: dgrad + mask/partials, one-split weight gradient,
+    finalize, dgrad with the BN-backward prologue, one-split weight gradient)."""
     from simclr_amd.parallel import state as pstate
     from simclr_amd.parallel.flat import FlatParamStore
     pstate.reset()
@@ -137,7 +137,7 @@ def test_fused_head_cuts_launches():
     k_fused = _head_kernels(m, x, R, S, True)
     k_ops = _head_kernels(m, x, R, S, False)
     print("head kernels fused / per-op:", k_fused, k_ops)
-    assert k_fused <= 9 and 10 * k_fused <= 6 * k_ops, (k_fused, k_ops)
+    assert k_fused <= 10 and 10 * k_fused <= 6 * k_ops, (k_fused, k_ops)
 
 
 def test_capture_without_warmup_skips_plan_build():
@@ -183,3 +183,36 @@ def test_capture_without_warmup_skips_plan_build():
     torch.cuda.synchronize()
     assert _rel(z_cap2, z_eager) < 1e-2
     del store
+
+
+@pytest.mark.parametrize("M,K,N,ks,seg", [(1024, 2048, 128, 16, 512), (512, 1024, 64, 4, 256),
+                                          (256, 512, 128, 2, 256)])
+def test_gemm_splitk_matches_fp32(M, K, N, ks, seg):
+    """The projection head's split-K GEMM 2 (misc.hip k_gemm_sk): relu(bn(y1)) · W2ᵀ + b2 with
+    per-segment scale / shift, against fp32 torch on the same bf16 operands; and with no
+    prologue; bitwise repeatable."""
+    from simclr_amd.ops import _ext
+    ops = _ext.ops()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(M + K)
+    S = M // seg
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    B = (torch.randn(N, K, device=dev) * 0.03).to(torch.bfloat16)
+    sc = (0.5 + torch.rand(S, K, device=dev)).contiguous()
+    sh = (torch.randn(S, K, device=dev) * 0.3).contiguous()
+    bias = torch.randn(N, device=dev)
+    part = torch.empty(ks * M * N, device=dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm_sk(A, B, sc.view(-1), sh.view(-1), seg, ks, part, bias, out)
+    sg = torch.arange(M, device=dev) // seg
+    Ap = torch.relu(A.float() * sc[sg] + sh[sg]).to(torch.bfloat16).float()
+    ref = Ap @ B.float().t() + bias
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < 5e-3, err
+    out2 = torch.empty_like(out)
+    ops.gemm_sk(A, B, sc.view(-1), sh.view(-1), seg, ks, part, bias, out2)
+    assert torch.equal(out, out2)
+    ops.gemm_sk(A, B, None, None, seg, ks, part, None, out)
+    ref = A.float() @ B.float().t()
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 5e-3
+
