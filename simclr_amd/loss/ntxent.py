@@ -111,7 +111,7 @@ class _NTXentHipFn(torch.autograd.Function):
                 # the head gathered z view by view on this side stream, under its GEMM 2
                 zb_all, pre_keep = pre
             else:
-                pre_keep = None
+                pre_keep = pre  # (a mismatched pre-gather's buffers: still in use on the side stream)
                 zb_all = torch.empty((Ccols, D), device=dev, dtype=torch.bfloat16)
                 with torch.cuda.stream(side):
                     ipc = getattr(st, "ipc", None)
