@@ -19,7 +19,6 @@ concat copies, no host→device target upload per call).  CPU / fp32 path: torch
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -178,21 +177,9 @@ class _NTXentHipFn(torch.autograd.Function):
         s_col = ops.nt_bwd_splits(Ccols, R)
         part2 = torch.empty((s_col * Ccols * D,), device=dev, dtype=torch.float32)
         d_cols = torch.empty((Ccols, D), device=dev, dtype=torch.float32)
+        ops.nt_backward_part(False, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part2,
+                             s_col, d_cols)
         overlap = gather and st.comm and dev.type == "cuda"
-        # local loss on a GPU: the column-gradient kernel on the side stream beside the row-
-        # gradient kernel (independent; each reads the forward's tables), joined before the sum
-        local_par = (not (gather and st.comm) and dev.type == "cuda"
-                     and os.environ.get("SIMCLR_NTXENT_BWD_PAR", "1") != "0")
-        if local_par:
-            cur = torch.cuda.current_stream(dev)
-            side = _side_stream(dev)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                ops.nt_backward_part(False, zall, znT, lse, R, col_offset, n, inv_t, scale, g,
-                                     part2, s_col, d_cols)
-        else:
-            ops.nt_backward_part(False, zall, znT, lse, R, col_offset, n, inv_t, scale, g, part2,
-                                 s_col, d_cols)
         if overlap:
             # global negatives: only this rank's slice of the column gradient is needed, so a
             # reduce-scatter (1/W of an all-reduce's bytes over xGMI) — issued on a side stream
@@ -222,8 +209,6 @@ class _NTXentHipFn(torch.autograd.Function):
             dist.reduce_scatter_tensor(mine, d_cols, group=st.group)
             d_rows += mine
         else:
-            if local_par:
-                cur.wait_stream(side)  # (part2 / d_cols stay referenced until here)
             d_rows += d_cols[col_offset:col_offset + R]
         if zdtype == torch.bfloat16:
             dz = torch.empty((R, D), device=dev, dtype=torch.bfloat16)
